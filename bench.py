@@ -1,0 +1,185 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ray-samples/s of one fwd+bwd training step (BASELINE.json `metric`).
+
+Workload (BASELINE.json configs[2]): synthetic Lego-style 400x400 camera,
+4096 rays x 64 samples per GPU, positional encoding F=5 (33 inputs), MLP 33->256x7->4, fp32,
+random-init weights (mlp_utils.py:166-204, seed 215). A step = positional encoding + MLP forward
++ compositing + sum-of-squares loss + the reverse pass over every MLP weight (the work of one
+nerf_evaluate_and_march + grad_nerf_evaluate_and_march pair on the batch), on inputs already
+resident in HBM. With N > 1 GPUs (one process per GPU, torchrun) every rank runs its own 4096-ray
+batch (weak scaling) and the packed [dW, db, loss] buffer is all-reduced (SUM) over RCCL, then
+scaled by the global loss (the reference seeds its gradient with the loss, train_nerf.py:477).
+
+Prints one JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "loma-nerf_amd"))
+
+METRIC = "ray-samples/sec fwd+bwd, 4096 rays×64 samples, 1/2/4/8 MI355X"
+PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA = f32 vector peak (dense)
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="cfg3")
+    ap.add_argument("--rays", type=int, default=None, help="rays per GPU (default: config)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-rays", type=int, default=16, help="rays in the CPU-baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--generic", action="store_true", help="time the loma-order kernels instead")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, cfg):
+    """The C oracle (loma-order scalar fp32 restatement, -O2, no FMA) timed on this host on a
+    bounded sample of the same workload. Test infrastructure, used only as the reported baseline."""
+    sys.path.insert(0, os.path.join(HERE, "oracle"))
+    import numpy as np
+    import oracle
+    import scene
+    b = scene.make_batch(cfg, rays=args.cpu_rays)
+    shapes, wp, bp = scene.init_mlp(3 + 6 * b["F"], 4, b["L"], b["H"])
+    X = oracle.positional_encoding_3d(b["pts"].astype(np.float64), b["F"])
+    res = {}
+    for threads, rays in ((1, args.cpu_rays), (args.cpu_threads, args.cpu_rays * args.cpu_threads)):
+        bb = scene.make_batch(cfg, rays=rays)
+        Xb = oracle.positional_encoding_3d(bb["pts"].astype(np.float64), bb["F"])
+        oracle.train_step(Xb[: 2 * bb["S"]], wp, bp, shapes, bb["dists"][:2], bb["target"][:2],
+                          bb["S"], threads=1)  # warm the library
+        t0 = time.perf_counter()
+        oracle.train_step(Xb, wp, bp, shapes, bb["dists"], bb["target"], bb["S"], threads=threads)
+        dt = time.perf_counter() - t0
+        res[threads] = (rays * bb["S"] / dt, rays, dt)
+    del X
+    v1, r1, t1 = res[1]
+    vn, rn, tn = res[args.cpu_threads]
+    return ({"value": v1, "unit": "ray-samples/s", "cores": 1, "kind": "port",
+             "sample": f"{r1} rays x {b['S']} samples of {cfg}, one fwd+grad step, scalar "
+                       f"loma-order C oracle (-O2, no FMA), {t1:.1f}s"},
+            {"value": vn, "unit": "ray-samples/s", "cores": args.cpu_threads, "kind": "port",
+             "sample": f"{rn} rays x {b['S']} samples, OpenMP over rays, {tn:.1f}s"})
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import torch
+    import lnerf
+    import scene
+
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = f"cuda:{local}"
+    b = scene.make_batch(args.config, rays=args.rays, rank=rank)
+    shapes, wp, bp = scene.init_mlp(3 + 6 * b["F"], 4, b["L"], b["H"])
+    N, S = b["N"], b["S"]
+    eng = lnerf.Engine(local)
+    mlp = lnerf.make_mlp(shapes, wp.shape[1], wp.shape[2])
+    ws = torch.from_numpy(wp).to(dev)
+    bs = torch.from_numpy(bp).to(dev)
+    pts = torch.from_numpy(b["pts"]).to(dev)
+    dists = torch.from_numpy(b["dists"]).to(dev)
+    target = torch.from_numpy(b["target"]).to(dev)
+    grads = eng.alloc_grads(len(shapes), wp.shape[1], wp.shape[2])
+    gbuf = grads[0]
+    acc = torch.empty(N, 3, device=dev)
+    flags = lnerf.GENERIC if args.generic else lnerf.FAST
+
+    def step(timing=False):
+        f = flags | (lnerf.TIMING if timing else 0)
+        if world == 1:
+            eng.train_step(mlp, ws, bs, pts, dists, target, samples=S, num_freqs=b["F"],
+                           seed=None, flags=f, grads=grads, acc_color=acc)
+        else:
+            eng.train_step(mlp, ws, bs, pts, dists, target, samples=S, num_freqs=b["F"],
+                           seed=1.0, flags=f, grads=grads, acc_color=acc)
+            dist.all_reduce(gbuf)                      # [dW, db, loss] SUM over ranks (RCCL)
+            eng.scale_by_device_scalar(gbuf[:-1], gbuf[-1:])
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms = dt / args.steps * 1e3
+    value = world * N * S / (ms / 1e3)
+
+    # per-kernel HIP-event times over extra timed steps (same stream, same kernels)
+    kt = {}
+    if not args.generic:
+        reps = max(3, min(args.steps, 10))
+        acc_t = {}
+        for _ in range(reps):
+            step(timing=True)
+            for k, v in eng.timings().items():
+                acc_t[k] = acc_t.get(k, 0.0) + v
+        kt = {k: v / reps for k, v in acc_t.items()}
+    fused_flops = scene.fused_kernel_flops(shapes) * N * S
+    dw_flops = scene.dw_kernel_flops(shapes) * N * S
+    step_flops = scene.step_flops(shapes) * N * S
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": value, "unit": "ray-samples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (look-at camera rays, uniform targets, random-init MLP seed 215)",
+            "config": {"workload": f"{args.config}: {N} rays x {S} samples per GPU, PE F={b['F']}, "
+                                   f"MLP {shapes[0][0]}->{b['H']}x{b['L'] - 1}->4, fp32",
+                       "rays_per_gpu": N, "samples": S, "layers": b["L"], "width": b["H"],
+                       "parallelism": f"dp{world}", "path": "generic" if args.generic else "fused"},
+            "step_tflops": step_flops / (ms / 1e3) / 1e12,
+        }
+        if kt:
+            fus_ms = kt["fused"]
+            out["roofline"] = {"bound": "mfma", "kernel": "fused_fwd_bwd_kernel",
+                               "achieved": fused_flops / (fus_ms / 1e3) / 1e12,
+                               "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                               "frac": fused_flops / (fus_ms / 1e3) / 1e12 / PEAK_FP32_TFLOPS,
+                               "traffic": None,
+                               "flops_per_launch": fused_flops, "avg_ms": fus_ms}
+            out["kernels_ms"] = kt
+            out["dw_kernel_tflops"] = dw_flops / (kt["dw"] / 1e3) / 1e12
+        if world == 1 and not args.no_cpu_baseline:
+            c1, cn = cpu_baseline(args, args.config)
+            out["cpu_baseline"] = c1
+            out["cpu_baseline_mt"] = cn
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,176 @@
+/*
+ * lnerf.h -- C ABI of libloma_nerf.so, the MI355X-native NeRF ray-marching engine.
+ *
+ * Two levels, both exported by the same library (see INTEGRATION.md for the bindings):
+ *
+ *  (1) loma-compat entry points with the exact signatures loma's C target generates for
+ *      scripts/nerf.py and scripts/mlp_fit.py (codegen_c.py:8-30,47-57; reverse_diff.py:504-517).
+ *      Arrays are nested host pointer tables (mlp_utils.py:33-118), exactly what ctypes passes.
+ *      They gather into pinned memory, run the HIP kernels on the calling thread's stream and
+ *      scatter the results back, with loma's semantics.
+ *
+ *  (2) the native batched API on device-resident, contiguous buffers (the throughput path).
+ *
+ * No torch or HIP types appear here: streams are passed as `void*` (a hipStream_t, NULL = the
+ * calling thread's default engine stream). Every entry point returns 0 on success / a negative
+ * error code, or (loma-compat float returns) NaN on failure; lnerf_last_error() describes it.
+ */
+#ifndef LNERF_H
+#define LNERF_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LNERF_MAX_LAYERS 16
+
+/* ------------------------------------------------------------------------------------------ */
+/* (1) loma-compat ABI                                                                          */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Replaces the loma-generated `nerf_evaluate_and_march` (scripts/nerf.py:1-304, bound at
+ * train_nerf.py:212 and called at :325 and :616). Returns the sum-of-squares loss. */
+float nerf_evaluate_and_march(float** layer_input, int layer_input_h, int layer_input_w,
+                              float*** ws, float** bs, float** target_image, int target_image_h,
+                              int target_image_w, int num_weights, int** weight_shapes,
+                              int** bias_shapes, int** intermediate_output_shapes,
+                              float*** intermediate_outputs, float*** img_sample_rgba_arr,
+                              int num_samples, float** dists, float** alpha,
+                              float** cumprod_alpha, float** weights_samples,
+                              float** accumulated_color);
+
+/* Replaces `grad_nerf_evaluate_and_march = rev_diff(nerf_evaluate_and_march)`
+ * (scripts/nerf.py:306, bound at train_nerf.py:213, called at :395-478). Every In array is
+ * followed by its adjoint buffer, every In int by an int* adjoint (never written), and the last
+ * argument is the seed `_dreturn` (reverse_diff.py:504-517). Adjoint buffers are accumulated
+ * into; primal buffers are left unchanged. */
+void grad_nerf_evaluate_and_march(
+    float** layer_input, float** d_layer_input, int layer_input_h, int* d_layer_input_h,
+    int layer_input_w, int* d_layer_input_w, float*** ws, float*** d_ws, float** bs,
+    float** d_bs, float** target_image, float** d_target_image, int target_image_h,
+    int* d_target_image_h, int target_image_w, int* d_target_image_w, int num_weights,
+    int* d_num_weights, int** weight_shapes, int** d_weight_shapes, int** bias_shapes,
+    int** d_bias_shapes, int** intermediate_output_shapes, int** d_intermediate_output_shapes,
+    float*** intermediate_outputs, float*** d_intermediate_outputs,
+    float*** img_sample_rgba_arr, float*** d_img_sample_rgba_arr, int num_samples,
+    int* d_num_samples, float** dists, float** d_dists, float** alpha, float** d_alpha,
+    float** cumprod_alpha, float** d_cumprod_alpha, float** weights_samples,
+    float** d_weights_samples, float** accumulated_color, float** d_accumulated_color,
+    float _dreturn);
+
+/* Replaces loma's `mlp_fit` (scripts/mlp_fit.py:1-147; fit_img.py:359,515-530). `layer_output`
+ * is unused, as in the reference. */
+float mlp_fit(float** layer_input, int layer_input_h, int layer_input_w, float** layer_output,
+              float*** ws, float** bs, float** target_image, int target_image_h,
+              int target_image_w, int num_weights, int** weight_shapes, int** bias_shapes,
+              int** intermediate_output_shapes, float*** intermediate_outputs);
+
+/* Replaces `grad_mlp_fit = rev_diff(mlp_fit)` (scripts/mlp_fit.py:174; fit_img.py:361,468-498). */
+void grad_mlp_fit(float** layer_input, float** d_layer_input, int layer_input_h,
+                  int* d_layer_input_h, int layer_input_w, int* d_layer_input_w,
+                  float** layer_output, float** d_layer_output, float*** ws, float*** d_ws,
+                  float** bs, float** d_bs, float** target_image, float** d_target_image,
+                  int target_image_h, int* d_target_image_h, int target_image_w,
+                  int* d_target_image_w, int num_weights, int* d_num_weights,
+                  int** weight_shapes, int** d_weight_shapes, int** bias_shapes,
+                  int** d_bias_shapes, int** intermediate_output_shapes,
+                  int** d_intermediate_output_shapes, float*** intermediate_outputs,
+                  float*** d_intermediate_outputs, float _dreturn);
+
+/* Replaces loma's `mult_a_b` (scripts/mlp_fit.py:150-172; fit_img.py:360,370). */
+void mult_a_b(float** a, int a_h, int a_w, float** b, int b_h, int b_w, float** c);
+
+/* ------------------------------------------------------------------------------------------ */
+/* (2) native batched API (device pointers)                                                    */
+/* ------------------------------------------------------------------------------------------ */
+
+typedef struct lnerf_ctx lnerf_ctx;
+
+/* MLP shape. Weights use the reference's padded layout (mlp_utils.py:272-313): ws[l][k][j] at
+ * ws[(l*w_k + k)*w_n + j], bs[l][j] at bs[l*w_n + j]; layer l maps k[l] -> n[l] features,
+ * ReLU on hidden layers, head = sigmoid(rgb) + ReLU(sigma) (scripts/nerf.py:134-167). */
+typedef struct {
+    int num_layers;
+    int k[LNERF_MAX_LAYERS];
+    int n[LNERF_MAX_LAYERS];
+    int w_k, w_n;
+} lnerf_mlp;
+
+enum {
+    LNERF_INPUT_ENCODED = 0, /* x = layer_input, (rays*S, k[0]) float32 row-major          */
+    LNERF_INPUT_POINTS = 1   /* x = sample positions, (rays*S, 3) float32; the engine      */
+                             /*     applies positional_encoding_3d (pos_encoding.py:38-69)  */
+};
+
+/* One batch of rays; all pointers are device pointers. Sample r of ray i is row i*S + r
+ * (train_nerf.py:327). */
+typedef struct {
+    int rays;
+    int samples;         /* S */
+    int input_mode;      /* LNERF_INPUT_* */
+    int num_freqs;       /* F (POINTS mode; k[0] must equal 3 + 6F) */
+    const float* x;
+    const float* dists;  /* (rays, S) delta t, last = 1e8 in the reference (train_nerf.py:306) */
+    const float* target; /* (rays, 3) */
+} lnerf_batch;
+
+enum {
+    LNERF_SEED_CONST = 0,     /* gradients seeded with `seed`                                 */
+    LNERF_SEED_LOSS = 1,      /* seeded with the batch loss itself (train_nerf.py:477)        */
+    LNERF_ACCUMULATE = 2,     /* add into d_ws/d_bs (loma semantics) instead of overwriting   */
+    LNERF_WANT_DX = 4,        /* also produce d_x (d_layer_input), ENCODED mode only          */
+    LNERF_GENERIC = 8,        /* force the stage-by-stage loma-order kernels (no MFMA fusion) */
+    LNERF_FAST = 16,          /* require the fused MFMA path (error if the shape is unsupported) */
+    LNERF_TIMING = 32         /* record per-kernel HIP events (read with lnerf_ctx_timings)   */
+};
+
+/* Optional outputs (device pointers; any may be NULL). */
+typedef struct {
+    float* loss;         /* 1 float                                     */
+    float* acc_color;    /* (rays, 3)                                   */
+    float* d_ws;         /* (L, w_k, w_n) padded                        */
+    float* d_bs;         /* (L, w_n)                                    */
+    float* d_x;          /* (rays*S, k[0]) with LNERF_WANT_DX           */
+    float* d_dists;      /* (rays, S)                                   */
+    float* d_target;     /* (rays, 3)                                   */
+} lnerf_outputs;
+
+const char* lnerf_last_error(void);
+const char* lnerf_version(void);
+
+int lnerf_ctx_create(lnerf_ctx** out, int device);
+void lnerf_ctx_destroy(lnerf_ctx* ctx);
+/* Bytes of device workspace a train step needs (activation slabs, partials). */
+size_t lnerf_workspace_bytes(const lnerf_mlp* mlp, int rays, int samples);
+
+/* Forward (PE + MLP + compositing + loss) and reverse pass over the MLP weights: the work of one
+ * nerf_evaluate_and_march + grad_nerf_evaluate_and_march pair on the whole batch. */
+int lnerf_train_step(lnerf_ctx* ctx, const lnerf_mlp* mlp, const float* ws, const float* bs,
+                     const lnerf_batch* batch, float seed, int flags, const lnerf_outputs* out,
+                     void* stream);
+
+/* Forward only (eval render, train_nerf.py:616-661): acc_color and, if target != NULL, loss. */
+int lnerf_render(lnerf_ctx* ctx, const lnerf_mlp* mlp, const float* ws, const float* bs,
+                 const lnerf_batch* batch, const lnerf_outputs* out, void* stream);
+
+/* Per-kernel times (ms) of the last LNERF_TIMING step on `ctx`, measured with HIP events on the
+ * step's stream: [0] weight pack, [1] fused fwd+reverse-chain kernel, [2] loss reduce,
+ * [3] dW kernel, [4] dW/db reduce, [5] whole step. Synchronises on the step. Returns the number
+ * of values written (0 if no timed step ran on the fused path). */
+int lnerf_ctx_timings(lnerf_ctx* ctx, float* ms_out, int n);
+
+/* buf[i] *= *scale for i < n (device pointers): applies a loss seed after an all-reduce of
+ * unit-seeded gradients (the data-parallel path). */
+int lnerf_scale_by_device_scalar(float* buf, size_t n, const float* scale, void* stream);
+
+/* The reference's Adam (train_nerf.py:133-161) on device: params -= lr_t m_hat/(sqrt(v_hat)+eps).
+ * `t` is the 1-based step count after the increment. */
+int lnerf_adam_update(float* params, const float* grads, float* m, float* v, size_t n, int t,
+                      float lr, float beta1, float beta2, float eps, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LNERF_H */

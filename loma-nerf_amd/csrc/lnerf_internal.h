@@ -1,0 +1,130 @@
+// lnerf_internal.h -- shared declarations between the HIP kernels and the C-ABI layer.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "lnerf.h"
+
+namespace lnerf {
+
+constexpr int kMaxLayers = LNERF_MAX_LAYERS;
+
+// ----------------------------------------------------------------------------------------------
+// Generic ("loma-order") path: one loma call on flat device rectangles. Field meaning follows
+// scripts/nerf.py:1-22; loop bounds are exactly the reference's.
+// ----------------------------------------------------------------------------------------------
+struct LgDims {
+    int L;                    // num_weights
+    int in_h, in_w;           // layer_input_h / layer_input_w
+    int th, tw;               // target_image_h / target_image_w
+    int S;                    // num_samples
+    int wsh1[kMaxLayers];     // weight_shapes[l][1]
+    int ios0[kMaxLayers];     // intermediate_output_shapes[l][0]
+    int ios1[kMaxLayers];     // intermediate_output_shapes[l][1]
+    int x_cols;               // strides of the flat rectangles
+    int w_k, w_n, b_n;
+    int io_rows, io_cols;
+    int t_cols, acc_cols;
+    int nerf_head;            // 1: nerf.py head (sigma ReLU on channel 3); 0: mlp_fit (all sigmoid)
+};
+
+struct LgBuffers {
+    // primal (device)
+    const float* X;
+    const float* W;
+    const float* B;
+    const float* T;
+    float* IO;      // intermediate_outputs, mutated in place
+    float* rgba;    // (th, S, 4)
+    const float* dists;
+    float* alpha;
+    float* cp;
+    float* wsamp;
+    float* acc;     // (th, acc_cols)
+    // snapshots for the reverse sweep (nullable in a forward-only call)
+    float* zpre;    // io right after each layer's bias stage
+    float* cpC;     // cumprod buffer after its init stage (c_j)
+    float* cpP;     // after the inclusive product (P_j)
+};
+
+struct LgAdjoints {
+    float* dX;      // nullable
+    float* dW;
+    float* dB;
+    float* dT;
+    float* dIO;
+    float* drgba;
+    float* ddists;
+    float* dalpha;
+    float* dcp;
+    float* dwsamp;
+    float* dacc;
+};
+
+// nerf_evaluate_and_march on device; writes the loss to *loss_dev.
+void lg_nerf_forward(const LgDims& d, const LgBuffers& b, float* loss_dev, hipStream_t s);
+// grad_nerf_evaluate_and_march: b must hold a *fresh copy* of the primal inputs (the forward is
+// re-executed on it, snapshots filled); adjoints accumulate in `a`. `seed_dev` is a device
+// scalar (so the seed may be a loss computed on the device).
+void lg_nerf_grad(const LgDims& d, const LgBuffers& b, const LgAdjoints& a, const float* seed_dev,
+                  hipStream_t s);
+void lg_mlp_fit_forward(const LgDims& d, const LgBuffers& b, float* loss_dev, hipStream_t s);
+void lg_mlp_fit_grad(const LgDims& d, const LgBuffers& b, const LgAdjoints& a,
+                     const float* seed_dev, hipStream_t s);
+void lg_mult_a_b(const float* a, int a_h, int a_w, const float* b, int b_w, float* c,
+                 hipStream_t s);
+
+// small helpers
+void k_fill(float* p, float v, size_t n, hipStream_t s);
+void k_scale_by_scalar(float* p, size_t n, const float* scale, hipStream_t s);
+void k_positional_encoding(const float* pts, int n, int F, float* out, int out_cols,
+                           hipStream_t s);
+void k_adam(float* params, const float* grads, float* m, float* v, size_t n, int t, float lr,
+            float beta1, float beta2, float eps, hipStream_t s);
+
+// ----------------------------------------------------------------------------------------------
+// Fused MFMA path (the throughput path). See DESIGN.md "Kernels".
+// ----------------------------------------------------------------------------------------------
+struct FusedPlan {
+    int L;
+    int k[kMaxLayers], n[kMaxLayers];   // real widths
+    int kt[kMaxLayers], nt[kMaxLayers]; // 32-wide tiles
+    int w_k, w_n;
+    int rays, S, R;                     // R = rays*S
+    int rays_per_wg;                    // whole rays per 128-sample workgroup tile
+    int num_wg;                         // fused-kernel grid
+    int blocks;                         // 32-sample slabs = num_wg * 4
+    int input_mode, F;
+    // workspace carve (device pointers)
+    float* wf;        // forward-packed weights, per layer offsets below
+    float* wb;        // backward-packed weights
+    float* bp;        // biases in fragment order
+    size_t wf_off[kMaxLayers], wb_off[kMaxLayers], bp_off[kMaxLayers];
+    float* act;       // activation slabs: layer l at act_off[l] (l = -1 -> input X slab at x_off)
+    size_t act_off[kMaxLayers];
+    float* grad;      // gradient slabs G_l at grad_off[l]
+    size_t grad_off[kMaxLayers];
+    float* loss_part; // per-workgroup partial loss (num_wg)
+    float* dw_part;   // dW split partials
+    float* db_part;   // dB split partials
+    int dw_splits[kMaxLayers];
+    int dw_split_off[kMaxLayers];  // workgroup offset of layer l in the dW grid
+    size_t dwp_off[kMaxLayers];    // float offset of layer l's partial slabs in dw_part
+    size_t dbp_off[kMaxLayers];
+    int dw_grid;
+    float* loss_total; // device scalar
+};
+
+bool fused_supported(const lnerf_mlp& mlp, int rays, int S, int input_mode, const char** why);
+size_t fused_workspace_bytes(const lnerf_mlp& mlp, int rays, int S);
+void fused_plan(FusedPlan& p, const lnerf_mlp& mlp, const lnerf_batch& b, void* ws_base);
+// ev: nullable array of 7 events recorded between the step's kernels (LNERF_TIMING)
+void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, const lnerf_batch& b,
+                      float seed, int flags, const lnerf_outputs& out, hipStream_t s,
+                      hipEvent_t* ev);
+void fused_render(const FusedPlan& p, const float* ws, const float* bs, const lnerf_batch& b,
+                  const lnerf_outputs& out, hipStream_t s);
+
+}  // namespace lnerf

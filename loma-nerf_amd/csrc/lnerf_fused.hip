@@ -312,7 +312,7 @@ __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs 
             const float* bo = bpl;  // tile 0, h = 0
             if (h == 0) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) comp[ls * kCompFloats + r] = out[0][r] + bo[r];
+                for (int r = 0; r < 4; ++r) comp[ls * 4 + r] = out[0][r] + bo[r];  // c_z[ls][r]
             }
         }
     }

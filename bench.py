@@ -36,7 +36,7 @@ def parse():
     ap.add_argument("--config", default="cfg3")
     ap.add_argument("--rays", type=int, default=None, help="rays per GPU (default: config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-rays", type=int, default=16, help="rays in the CPU-baseline sample")
+    ap.add_argument("--cpu-rays", type=int, default=128, help="rays in the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--generic", action="store_true", help="time the loma-order kernels instead")
     return ap.parse_args()

@@ -18,6 +18,7 @@
 #include "lnerf_internal.h"
 
 #include <math.h>
+#include <stdlib.h>
 
 namespace lnerf {
 
@@ -72,14 +73,20 @@ constexpr int kLdsW = 2 * kChunkMax;                                    // float
 constexpr int kLdsMaskU64 = kWaves * kMaxMaskLayers * kNT * 16;         // 64-bit words
 constexpr int kLdsComp = kTileSamples * kCompFloats;                    // floats
 constexpr int kLdsRay = kTileSamples;                                   // per-ray loss partials
+constexpr int kLdsTr = kWaves * 32 * 32;                                // per-wave transpose tile
+constexpr int kLdsBias = 2 * kNT * 32;                                  // 2 x one layer's biases
 constexpr size_t kLdsBytes = (size_t)kLdsW * 4 + (size_t)kLdsMaskU64 * 8 + (size_t)kLdsComp * 4 +
-                             (size_t)kLdsRay * 4;
+                             (size_t)kLdsRay * 4 + (size_t)kLdsTr * 4 + (size_t)kLdsBias * 4;
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
+
+__device__ __forceinline__ int wave_id() {
+    return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
+}
 
 // Stage `cf` floats of packed weights into LDS with LDS-DMA (global_load_lds_dwordx4): lane-linear
 // destination, 1 KiB per wave instruction.
 __device__ __forceinline__ void stage_chunk(const float* __restrict__ src, float* dst, int cf) {
-    const int tid = threadIdx.x, wave = tid >> 6;
+    const int tid = threadIdx.x, wave = wave_id();
     for (int base = 0; base < cf; base += kWgThreads * 4) {
         const float* g = src + base + tid * 4;
         float* l = dst + base + wave * 256;
@@ -88,37 +95,78 @@ __device__ __forceinline__ void stage_chunk(const float* __restrict__ src, float
     }
 }
 
-// out[o] += sum_{c < nchunks, r} Wpack[c][r][o] (x) in[c][r], the packed weights of one layer
-// streamed chunk by chunk (chunk c = contraction tile c) through a 2-deep LDS ring.
-__device__ __forceinline__ void mma_stream(const float* __restrict__ src, int nchunks, int nto,
-                                           const fx16 (&in)[kNT], fx16 (&out)[kNT], float* ldsw) {
-    const int lane = threadIdx.x & 63;
-    const int nt4 = (nto + 3) >> 2;
-    const int cf = 16 * nt4 * 256;
-    stage_chunk(src, ldsw, cf);
+// Wait for this wave's LDS-DMA (and other vector-memory ops), then barrier: after it every wave's
+// staged bytes are in LDS (explicit, not left to __syncthreads' lowering).
+__device__ __forceinline__ void dma_barrier() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+}
+
+// Store one 32x32 accumulator tile (lane = sample, registers = features in C/D order) as a
+// row-major [feature][32 samples] block: transpose through the wave's LDS tile, then 4
+// global_store_dwordx4 per lane (each wave instruction writes 8 whole 128-B rows).
+__device__ __forceinline__ void store_tile(const fx16& v, float* __restrict__ dst, float* tr) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, sl = lane & 31;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tr[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + sl] = v[r];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int row = (lane >> 3) + 8 * q, c4 = (lane & 7) * 4;
+        const fx4 x = *(const fx4*)(tr + row * 32 + c4);
+        *(fx4*)(dst + row * 32 + c4) = x;
+    }
+}
+
+// out[o] += sum_{c < nchunks, r} Wpack[c][r][o] (x) in[c][r] for o < NTO: the packed weights of
+// one layer streamed chunk by chunk (chunk c = contraction tile c) through a 2-deep LDS ring.
+// NTO is compile-time and the chunk loop fully unrolled, so every register index is static (no
+// scratch, no per-MFMA branches); a chunk is skipped with one uniform branch.
+// While chunk c computes, input tile c-1 (already consumed) is written to its HBM slab
+// (`tstore`, nullable), so the slab stores drain under the MFMAs instead of stalling a barrier.
+// `bias_src` (nullable) = this layer's fragment-ordered biases, staged into `bias_lds`.
+template <int NTO>
+__device__ __forceinline__ void mma_stream_t(const float* __restrict__ src, int nchunks,
+                                             const fx16 (&in)[kNT], fx16 (&out)[kNT], float* ldsw,
+                                             float* tstore, float* tr, const float* bias_src,
+                                             float* bias_lds) {
+    const int lane = threadIdx.x & 63;
+    constexpr int NT4 = (NTO + 3) / 4;
+    constexpr int CF = 16 * NT4 * 256;
+    stage_chunk(src, ldsw, CF);
+    if (bias_src && wave_id() == 0)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bias_src + lane * 4),
+                                         (__attribute__((address_space(3))) void*)bias_lds, 16, 0, 0);
+    dma_barrier();
 #pragma unroll
     for (int c = 0; c < kNT; ++c) {
         if (c < nchunks) {
-            const float* cur = ldsw + (c & 1) * kChunkMax;
-            if (c + 1 < nchunks) stage_chunk(src + (size_t)(c + 1) * cf, ldsw + ((c + 1) & 1) * kChunkMax, cf);
+            if (tstore && c >= 1) store_tile(in[c - 1], tstore + (c - 1) * 1024, tr);
+            const float* cur = ldsw + (c & 1) * kChunkMax + lane * 4;
+            if (c + 1 < nchunks)
+                stage_chunk(src + (size_t)(c + 1) * CF, ldsw + ((c + 1) & 1) * kChunkMax, CF);
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                fx4 w0 = *(const fx4*)(cur + (r * nt4 + 0) * 256 + lane * 4);
-                fx4 w1 = {0.f, 0.f, 0.f, 0.f};
-                if (nt4 > 1) w1 = *(const fx4*)(cur + (r * nt4 + 1) * 256 + lane * 4);
-                const float b = in[c][r];
+                fx4 w[NT4];
 #pragma unroll
-                for (int o = 0; o < kNT; ++o) {
-                    if (o < nto) {
-                        const float a = (o < 4) ? w0[o & 3] : w1[o & 3];
-                        out[o] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, out[o], 0, 0, 0);
-                    }
-                }
+                for (int q = 0; q < NT4; ++q) w[q] = *(const fx4*)(cur + (r * NT4 + q) * 256);
+#pragma unroll
+                for (int o = 0; o < NTO; ++o)
+                    out[o] = __builtin_amdgcn_mfma_f32_32x32x2f32(w[o >> 2][o & 3], in[c][r], out[o], 0, 0, 0);
             }
-            __syncthreads();
+            dma_barrier();
+            if (tstore && c == nchunks - 1) store_tile(in[c], tstore + c * 1024, tr);
         }
     }
+}
+
+// Output-tile counts are rounded up to 1/2/4/8 (the padded tiles of the packed weights are zero).
+__device__ __forceinline__ void mma_stream(const float* __restrict__ src, int nchunks, int nto,
+                                           const fx16 (&in)[kNT], fx16 (&out)[kNT], float* ldsw,
+                                           float* tstore, float* tr) {
+    if (nto <= 1) mma_stream_t<1>(src, nchunks, in, out, ldsw, tstore, tr, nullptr, nullptr);
+    else if (nto <= 2) mma_stream_t<2>(src, nchunks, in, out, ldsw, tstore, tr, nullptr, nullptr);
+    else if (nto <= 4) mma_stream_t<4>(src, nchunks, in, out, ldsw, tstore, tr, nullptr, nullptr);
+    else mma_stream_t<8>(src, nchunks, in, out, ldsw, tstore, tr, nullptr, nullptr);
 }
 
 __device__ __forceinline__ float input_feature(const FusedArgs& a, int gs, bool valid, int f) {
@@ -150,7 +198,8 @@ struct RayScratch {
     float* gz;     // [S][4] output: dL/dz head
 };
 
-__device__ float composite_ray(const FusedArgs& a, int ray, const RayScratch& s, bool grad) {
+__device__ __forceinline__ float composite_ray(const FusedArgs& a, int ray, const RayScratch& s,
+                                             bool grad) {
     const int S = a.S;
     const float* dists = a.dists + (size_t)ray * S;
     // head activation (nerf.py:153-167): channel 3 ReLU, 0..2 sigmoid
@@ -247,14 +296,18 @@ __device__ float composite_ray(const FusedArgs& a, int ray, const RayScratch& s,
     return loss;
 }
 
+// HT = output tiles of every hidden layer (widths <= 32*HT); the head has <= 32 outputs.
+template <int HT>
 __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs a) {
     __shared__ __attribute__((aligned(16))) unsigned char lds_raw[kLdsBytes];
     float* ldsw = (float*)lds_raw;
     unsigned long long* masks = (unsigned long long*)(lds_raw + (size_t)kLdsW * 4);
     float* comp = (float*)(lds_raw + (size_t)kLdsW * 4 + (size_t)kLdsMaskU64 * 8);
     float* rayloss = comp + kLdsComp;
+    float* trall = rayloss + kLdsRay;
+    float* biasl = trall + kLdsTr;
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id(), h = lane >> 5;
     const int wg = blockIdx.x;
     const int ls = wave * 32 + (lane & 31);           // local sample 0..127
     const int tile_samples = a.rpw * a.S;
@@ -262,62 +315,72 @@ __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs 
     const bool valid = (ls < tile_samples) && (gs < a.R);
     const size_t blk = (size_t)wg * kWaves + wave;    // 32-sample slab index
     unsigned long long* wmask = masks + (size_t)wave * kMaxMaskLayers * kNT * 16;
+    float* tr = trall + wave * 1024;
+    const bool st = a.want_grad != 0;
 
     fx16 act[kNT], out[kNT];
-    // ---- layer-0 input: features in accumulator order, X slab for dW_0 ----
+    // ---- layer-0 input: features in accumulator order ----
+    // Each 32-feature tile is produced into a per-wave LDS scratch (the weight ring is free
+    // before the first layer) by a compact loop, then picked up in accumulator order.
+    float* pe = ldsw + (size_t)wave * (32 * 33);
+    const int tile_base = wg * tile_samples + wave * 32;
 #pragma unroll
     for (int t = 0; t < kNT; ++t) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) act[t][r] = 0.0f;
         if (t < a.kt[0]) {
-            float* xs = a.act + a.x_off + blk * (size_t)(a.kt[0] * 1024);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int f = frag_feature(t, r, h);
-                const float v = input_feature(a, gs, valid, f);
-                act[t][r] = v;
-                if (a.want_grad) xs[f * 32 + (lane & 31)] = v;
+            for (int e = lane; e < 32 * 32; e += 64) {
+                const int sl = e >> 5, ft = e & 31;
+                const int lsl = wave * 32 + sl;
+                const bool vs = (lsl < tile_samples) && (tile_base + sl < a.R);
+                pe[sl * 33 + ft] = input_feature(a, tile_base + sl, vs, 32 * t + ft);
             }
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < 16; ++r) act[t][r] = pe[(lane & 31) * 33 + (frag_feature(t, r, h) - 32 * t)];
+            __syncthreads();
         }
     }
 
     // ---- forward through the layers ----
     for (int l = 0; l < a.L; ++l) {
-        const int nto = a.nt[l];
 #pragma unroll
         for (int o = 0; o < kNT; ++o) out[o] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        mma_stream(a.wf + a.wf_off[l], a.kt[l], nto, act, out, ldsw);
-        const float* bpl = a.bp + a.bp_off[l];
+        // the input tiles of layer l are A_{l-1} (X for l = 0): stored while layer l computes
+        float* ts = !st ? nullptr
+                        : (l == 0 ? a.act + a.x_off + blk * (size_t)(a.kt[0] * 1024)
+                                  : a.act + a.act_off[l - 1] + blk * (size_t)(a.kt[l] * 1024));
+        float* bl = biasl + (l & 1) * (kNT * 32);
+        if (l < a.L - 1) mma_stream_t<HT>(a.wf + a.wf_off[l], a.kt[l], act, out, ldsw, ts, tr, a.bp + a.bp_off[l], bl);
+        else mma_stream_t<1>(a.wf + a.wf_off[l], a.kt[l], act, out, ldsw, ts, tr, a.bp + a.bp_off[l], bl);
         if (l < a.L - 1) {
-            float* as = a.act + a.act_off[l] + blk * (size_t)(nto * 1024);
 #pragma unroll
-            for (int o = 0; o < kNT; ++o) {
-                if (o < nto) {
-                    const float* bo = bpl + (o * 2 + h) * 16;
+            for (int o = 0; o < HT; ++o) {
+                unsigned long long m[16];
+                const float* bo = bl + (o * 2 + h) * 16;
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        float v = out[o][r] + bo[r];
-                        v = (v > 0.0f) ? v : 0.0f;               // ReLU nerf.py:141-144
-                        out[o][r] = v;
-                        const unsigned long long m = __ballot(v > 0.0f);
-                        if (lane == 0) wmask[((size_t)l * kNT + o) * 16 + r] = m;
-                        if (a.want_grad) as[frag_feature(o, r, h) * 32 + (lane & 31)] = v;
-                    }
+                for (int r = 0; r < 16; ++r) {
+                    float v = out[o][r] + bo[r];
+                    v = (v > 0.0f) ? v : 0.0f;               // ReLU nerf.py:141-144
+                    act[o][r] = v;
+                    m[r] = __ballot(v > 0.0f);
+                }
+                if (lane == 0) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) wmask[((size_t)l * kNT + o) * 16 + r] = m[r];
                 }
             }
 #pragma unroll
-            for (int o = 0; o < kNT; ++o) act[o] = out[o];
+            for (int o = HT; o < kNT; ++o) act[o] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         } else {
             // head pre-activations (features 0..3 live in regs 0..3 of lane half 0)
-            const float* bo = bpl;  // tile 0, h = 0
             if (h == 0) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) comp[ls * 4 + r] = out[0][r] + bo[r];  // c_z[ls][r]
+                for (int r = 0; r < 4; ++r) comp[ls * 4 + r] = out[0][r] + bl[r];  // c_z[ls][r]
             }
         }
     }
     __syncthreads();
-
 
     // ---- rendering + loss + rendering reverse: one thread per ray ----
     // comp (struct of arrays over the tile's 128 local samples; ray-major like the samples)
@@ -357,73 +420,70 @@ __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs 
     if (!a.want_grad) return;
 
     // ---- reverse chain: G_{L-1} from the head, then G_{l-1} = (W_l G_l) * 1[A_{l-1} > 0] ----
-    fx16 g[kNT], go[kNT];
+    // g (= G_l) is the input of the next reverse MMA, which writes it to its slab chunk by chunk.
+    fx16* g = act;
+    fx16* go = out;
 #pragma unroll
-    for (int t = 0; t < kNT; ++t) g[t] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int t = 0; t < kNT; ++t) act[t] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (h == 0 && valid) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) g[0][r] = c_gz[ls * 4 + r];
+        for (int r = 0; r < 4; ++r) act[0][r] = c_gz[ls * 4 + r];
     }
-    {
-        const int ntl = a.nt[a.L - 1];
-        float* gsl = a.grad + a.grad_off[a.L - 1] + blk * (size_t)(ntl * 1024);
-#pragma unroll
-        for (int o = 0; o < kNT; ++o)
-            if (o < ntl) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) gsl[frag_feature(o, r, h) * 32 + (lane & 31)] = g[o][r];
-            }
-    }
+    (void)g;
+    (void)go;
     for (int l = a.L - 1; l >= 1; --l) {
-        const int kto = a.kt[l];  // outputs: input features of layer l (= nt[l-1])
 #pragma unroll
-        for (int o = 0; o < kNT; ++o) go[o] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        mma_stream(a.wb + a.wb_off[l], a.nt[l], kto, g, go, ldsw);
-        float* gsl = a.grad + a.grad_off[l - 1] + blk * (size_t)(kto * 1024);
+        for (int o = 0; o < kNT; ++o) out[o] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        float* ts = a.grad + a.grad_off[l] + blk * (size_t)(a.nt[l] * 1024);
+        mma_stream_t<HT>(a.wb + a.wb_off[l], a.nt[l], act, out, ldsw, ts, tr, nullptr, nullptr);
 #pragma unroll
-        for (int o = 0; o < kNT; ++o) {
-            if (o < kto) {
+        for (int o = 0; o < HT; ++o) {
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const unsigned long long m = wmask[((size_t)(l - 1) * kNT + o) * 16 + r];
-                    const float v = ((m >> lane) & 1ull) ? go[o][r] : 0.0f;
-                    go[o][r] = v;
-                    gsl[frag_feature(o, r, h) * 32 + (lane & 31)] = v;
-                }
+            for (int r = 0; r < 16; ++r) {
+                const unsigned long long m = wmask[((size_t)(l - 1) * kNT + o) * 16 + r];
+                act[o][r] = ((m >> lane) & 1ull) ? out[o][r] : 0.0f;
             }
         }
 #pragma unroll
-        for (int o = 0; o < kNT; ++o) g[o] = go[o];
+        for (int o = HT; o < kNT; ++o) act[o] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     }
+    // act now holds G_0 (nt[0] tiles)
+    float* g0 = a.grad + a.grad_off[0] + blk * (size_t)(a.nt[0] * 1024);
     if (a.d_x) {
-        // d_layer_input = G_0 W_0^T (ENCODED mode), written row-major (rows = samples)
-        const int kto = a.kt[0];
+        // d_layer_input = G_0 W_0^T (ENCODED mode), written row-major (rows = samples); the MMA
+        // also writes G_0's slab
 #pragma unroll
-        for (int o = 0; o < kNT; ++o) go[o] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        mma_stream(a.wb + a.wb_off[0], a.nt[0], kto, g, go, ldsw);
+        for (int o = 0; o < kNT; ++o) out[o] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        mma_stream(a.wb + a.wb_off[0], a.nt[0], a.kt[0], act, out, ldsw, g0, tr);
         if (valid) {
 #pragma unroll
             for (int o = 0; o < kNT; ++o)
-                if (o < kto) {
+                if (o < a.kt[0]) {
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
                         const int f = frag_feature(o, r, h);
-                        if (f < a.k0) a.d_x[(size_t)gs * a.k0 + f] = go[o][r];
+                        if (f < a.k0) a.d_x[(size_t)gs * a.k0 + f] = out[o][r];
                     }
                 }
         }
+    } else {
+#pragma unroll
+        for (int o = 0; o < kNT; ++o)
+            if (o < a.nt[0]) store_tile(act[o], g0 + o * 1024, tr);
     }
 }
 
 // ---------------------------------------------------------------------------------------------
-// dW_l = sum_s A_{l-1}[:, s] G_l[:, s]^T over a split of the 32-sample slabs, fp32 MFMA.
-// Each workgroup stages one slab pair (A: KT*32 rows, G: NTo*32 rows, 32 samples each) into LDS
-// with a 33-float row pitch (conflict-free column reads), double-buffered through registers.
-// Waves own 4x4 blocks of 32x32 output tiles; when the layer has fewer than 4 blocks, waves split
-// the 16 sample pairs of a slab by phase and write separate partials.
+// dW_l = sum_s A_{l-1}[:, s] G_l[:, s]^T (+ db_l = sum_s G_l[:, s]) over a split of the 32-sample
+// slabs, fp32 MFMA. Each workgroup streams slab pairs (A: KT*32 feature rows, G: NTo*32 rows, 32
+// samples = 128 B per row) into a 2-deep LDS ring with LDS-DMA (global_load_lds_dwordx4). Rows
+// are stored with their 16-B chunks XOR-swizzled by ((row >> 1) & 7) -- applied to the per-lane
+// global source address, the LDS image stays lane-linear -- so the ds_read_b128 fragment reads
+// (one feature row, 4 consecutive samples per lane) are bank-conflict free. Waves own up to 4x4
+// blocks of 32x32 output tiles; partials are written per split (deterministic, no atomics).
 // ---------------------------------------------------------------------------------------------
-constexpr int kPitch = 33;
-constexpr int kDwStageFloats = 2 * kNT * 32 * kPitch;  // A + G rows of one slab pair
+constexpr int kDwRows = kNT * 32;                 // max feature rows per slab
+constexpr int kDwStageFloats = 2 * kDwRows * 32;  // A + G region of one ring slot
 
 struct DwArgs {
     int L;
@@ -439,56 +499,87 @@ struct DwArgs {
     size_t dwp_off[kMaxLayers];
     float* db_part;
     size_t dbp_off[kMaxLayers];
+    int dbg;  // ablation (LNERF_DW_MODE): 0 normal, 1 loads only, 2 compute only
 };
 
-__device__ __forceinline__ void dw_load_regs(fx4 (&regs)[16], const float* a_src, const float* g_src,
-                                             int a_floats, int g_floats) {
-    const int tid = threadIdx.x;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int e = (q * kWgThreads + tid) * 4;
-        if (e < a_floats) regs[q] = *(const fx4*)(a_src + e);
-        else if (e - a_floats < g_floats) regs[q] = *(const fx4*)(g_src + (e - a_floats));
+__device__ __forceinline__ int swz_chunk(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+// Stage one slab (`rows` x 32 floats) into `dst` (rows x 32, swizzled) with LDS-DMA.
+__device__ __forceinline__ void dw_stage(const float* __restrict__ src, float* dst, int rows,
+                                         int wave, int lane) {
+    // each wave instruction covers 8 rows (1 KiB); lane -> row 8i + (lane >> 3), LDS chunk lane & 7
+    for (int i = wave; i < rows / 8; i += kWaves) {
+        const int row = i * 8 + (lane >> 3);
+        const int c = swz_chunk(row, lane & 7);
+        const float* g = src + row * 32 + c * 4;
+        float* l = dst + i * 256;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                         (__attribute__((address_space(3))) void*)l, 16, 0, 0);
     }
 }
 
-__device__ __forceinline__ void dw_store_lds(const fx4 (&regs)[16], float* lds, int a_floats,
-                                             int g_floats) {
-    const int tid = threadIdx.x;
-    float* ga = lds + kNT * 32 * kPitch;  // G rows start after the A rows
+__device__ __forceinline__ fx4 dw_frag(const float* base, int row, int g, int h) {
+    // samples 8g + 4h .. 8g + 4h + 3 of feature row `row`
+    const int c = swz_chunk(row, 2 * g + h);
+    return *(const fx4*)(base + row * 32 + c * 4);
+}
+
+// One wave's TI x TJ block of 32x32 output tiles over one staged slab pair. Sample order inside
+// the contraction: step (g, u) pairs lane half h with sample 8g + 4h + u (same for A and G).
+template <int TI, int TJ>
+__device__ __forceinline__ void dw_block(const float* ca, const float* cg, int kb, int jb,
+                                         fx16 (&acc)[4][4]) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, rl = lane & 31;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int e = (q * kWgThreads + tid) * 4;
-        if (e < a_floats + g_floats) {
-            const bool isA = e < a_floats;
-            const int ee = isA ? e : e - a_floats;
-            const int row = ee >> 5, col = ee & 31;
-            float* d = (isA ? lds : ga) + row * kPitch + col;
-            d[0] = regs[q][0];
-            d[1] = regs[q][1];
-            d[2] = regs[q][2];
-            d[3] = regs[q][3];
-        }
+    for (int g = 0; g < 4; ++g) {
+        fx4 af[TI], bf[TJ];
+#pragma unroll
+        for (int i = 0; i < TI; ++i) af[i] = dw_frag(ca, (kb + i) * 32 + rl, g, h);
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) bf[j] = dw_frag(cg, (jb + j) * 32 + rl, g, h);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int i = 0; i < TI; ++i)
+#pragma unroll
+                for (int j = 0; j < TJ; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][u], bf[j][u], acc[i][j], 0, 0, 0);
+    }
+}
+
+__device__ __forceinline__ void dw_block_dispatch(int ti, int tj, const float* ca, const float* cg,
+                                                  int kb, int jb, fx16 (&acc)[4][4]) {
+    switch (ti * 4 + tj) {
+#define LNERF_DWB(I, J) \
+    case I * 4 + J: dw_block<I, J>(ca, cg, kb, jb, acc); break;
+        LNERF_DWB(1, 1) LNERF_DWB(1, 2) LNERF_DWB(1, 3) LNERF_DWB(1, 4)
+        LNERF_DWB(2, 1) LNERF_DWB(2, 2) LNERF_DWB(2, 3) LNERF_DWB(2, 4)
+        LNERF_DWB(3, 1) LNERF_DWB(3, 2) LNERF_DWB(3, 3) LNERF_DWB(3, 4)
+        LNERF_DWB(4, 1) LNERF_DWB(4, 2) LNERF_DWB(4, 3) LNERF_DWB(4, 4)
+#undef LNERF_DWB
+        default: break;
     }
 }
 
 __global__ void __launch_bounds__(kWgThreads, 1) dw_kernel(DwArgs a) {
     __shared__ __attribute__((aligned(16))) float lds[2 * kDwStageFloats];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-    // which layer / split
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // which layer / split (uniform)
     int l = 0;
     while (l + 1 < a.L && (int)blockIdx.x >= a.wg_off[l + 1]) ++l;
     const int sp = blockIdx.x - a.wg_off[l];
     const int KT = a.kt[l], NTo = a.nt[l];
-    const int nbk = (KT + 3) >> 2, nbj = (NTo + 3) >> 2, nblk = nbk * nbj;
-    const int P = (nblk >= kWaves) ? 1 : (kWaves / nblk);
-    const int myblk = wave % nblk, phase = wave / nblk;
-    const bool active = phase < P;
-    const int kb = (myblk / nbj) * 4, jb = (myblk % nbj) * 4;
+    const int nbj = (NTo + 3) >> 2, nblk = ((KT + 3) >> 2) * nbj;
+    const bool active = wave < nblk;
+    // idle waves (layers with < 4 tile blocks) repeat block 0 unconditionally and discard it:
+    // a branch around the MFMAs would make the compiler shuttle the accumulators out of AGPRs
+    const int kb = active ? (wave / nbj) * 4 : 0, jb = active ? (wave % nbj) * 4 : 0;
+    const int ti = min(4, KT - kb), tj = min(4, NTo - jb);
     const int splits = a.splits[l];
     const int per = (a.blocks + splits - 1) / splits;
-    const int b0 = sp * per, b1 = min(a.blocks, b0 + per);
-    const int a_floats = KT * 1024, g_floats = NTo * 1024;
+    const int b0 = min(a.blocks, sp * per), b1 = min(a.blocks, b0 + per);
+    const int a_rows = KT * 32, g_rows = NTo * 32;
     const float* A = a.act + a.a_off[l];
     const float* G = a.grad + a.g_off[l];
 
@@ -499,53 +590,41 @@ __global__ void __launch_bounds__(kWgThreads, 1) dw_kernel(DwArgs a) {
         for (int j = 0; j < 4; ++j) acc[i][j] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     float dbsum = 0.0f;
 
-    fx4 regs[16];
+    const bool do_load = a.dbg != 2, do_mma = a.dbg != 1;
     if (b0 < b1) {
-        dw_load_regs(regs, A + (size_t)b0 * a_floats, G + (size_t)b0 * g_floats, a_floats, g_floats);
-        dw_store_lds(regs, lds, a_floats, g_floats);
+        dw_stage(A + (size_t)b0 * a_rows * 32, lds, a_rows, wave, lane);
+        dw_stage(G + (size_t)b0 * g_rows * 32, lds + kDwRows * 32, g_rows, wave, lane);
     }
-    __syncthreads();
+    dma_barrier();
     for (int b = b0; b < b1; ++b) {
-        const float* cur = lds + ((b - b0) & 1) * kDwStageFloats;
-        if (b + 1 < b1)
-            dw_load_regs(regs, A + (size_t)(b + 1) * a_floats, G + (size_t)(b + 1) * g_floats,
-                         a_floats, g_floats);
+        float* cur = lds + ((b - b0) & 1) * kDwStageFloats;
+        if (b + 1 < b1 && do_load) {
+            float* nxt = lds + ((b + 1 - b0) & 1) * kDwStageFloats;
+            dw_stage(A + (size_t)(b + 1) * a_rows * 32, nxt, a_rows, wave, lane);
+            dw_stage(G + (size_t)(b + 1) * g_rows * 32, nxt + kDwRows * 32, g_rows, wave, lane);
+        }
         const float* ca = cur;
-        const float* cg = cur + kNT * 32 * kPitch;
-        if (active) {
-#pragma unroll 4
-            for (int q = phase; q < 16; q += P) {
-                const int s = 2 * q + h;
-                float af[4], bf[4];
+        const float* cg = cur + kDwRows * 32;
+        // full 4x4 blocks: rows past the staged slab read stale LDS, those tiles are never written
+        if (do_mma) dw_block<4, 4>(ca, cg, kb, jb, acc);
+        if (tid < g_rows) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    af[i] = (kb + i < KT) ? ca[((kb + i) * 32 + (lane & 31)) * kPitch + s] : 0.0f;
-                    bf[i] = (jb + i < NTo) ? cg[((jb + i) * 32 + (lane & 31)) * kPitch + s] : 0.0f;
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        if (kb + i < KT && jb + j < NTo)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+            for (int c = 0; c < 8; ++c) {
+                const fx4 v = *(const fx4*)(cg + tid * 32 + swz_chunk(tid, c) * 4);
+                dbsum += (v[0] + v[1]) + (v[2] + v[3]);
             }
         }
-        if (tid < NTo * 32) {
-#pragma unroll 8
-            for (int s = 0; s < 32; ++s) dbsum += cg[tid * kPitch + s];
-        }
-        if (b + 1 < b1) dw_store_lds(regs, lds + ((b + 1 - b0) & 1) * kDwStageFloats, a_floats, g_floats);
-        __syncthreads();
+        dma_barrier();
     }
-    // partial slab: [split*P + phase][k][j], k < KT*32, j < NTo*32
+    // partial slab: [split][k][j], k < KT*32, j < NTo*32
     if (active) {
         const int ncol = NTo * 32;
-        float* part = a.dw_part + a.dwp_off[l] + (size_t)(sp * P + phase) * (KT * 32) * ncol;
+        float* part = a.dw_part + a.dwp_off[l] + (size_t)sp * (KT * 32) * ncol;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                if (kb + i < KT && jb + j < NTo) {
+                if (i < ti && j < tj) {
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
                         const int k = (kb + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -554,7 +633,7 @@ __global__ void __launch_bounds__(kWgThreads, 1) dw_kernel(DwArgs a) {
                     }
                 }
     }
-    if (tid < NTo * 32) a.db_part[a.dbp_off[l] + (size_t)sp * (NTo * 32) + tid] = dbsum;
+    if (tid < g_rows) a.db_part[a.dbp_off[l] + (size_t)sp * g_rows + tid] = dbsum;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -716,17 +795,17 @@ void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S) {
     off = 0;
     for (int l = 0; l < L; ++l) { y.grad_off[l] = off; off += (size_t)y.blocks * nt[l] * 1024; }
     y.grad_total = off;
-    // dW grid: ~32 splits for a full 8x8-tile layer, proportionally fewer for small layers
+    // dW grid: every workgroup runs full 4x4-tile wave blocks over its slabs, so a workgroup's time
+    // is set by its slab count alone -> give every layer the same split count, one wave of
+    // workgroups over the 256 CUs (1 workgroup per CU: 128 KiB of LDS).
     int wg = 0;
     size_t dwp = 0, dbp = 0;
     for (int l = 0; l < L; ++l) {
-        const int tiles = kt[l] * nt[l];
-        int sp = (32 * tiles + 63) / 64;
+        int sp = 256 / L;
         sp = sp < 1 ? 1 : sp;
         sp = sp > y.blocks ? y.blocks : sp;
-        const int nblk = ((kt[l] + 3) / 4) * ((nt[l] + 3) / 4);
         y.splits[l] = sp;
-        y.phases[l] = nblk >= kWaves ? 1 : kWaves / nblk;
+        y.phases[l] = 1;
         y.wg_off[l] = wg;
         wg += sp;
         y.dwp_off[l] = dwp;
@@ -747,6 +826,7 @@ bool fused_supported(const lnerf_mlp& m, int rays, int S, int input_mode, const 
     else if (S < 1 || S > kTileSamples) w = "fused path needs 1 <= samples <= 128";
     else if (rays < 1) w = "no rays";
     else if (m.n[m.num_layers - 1] < 4) w = "head must have >= 4 outputs (rgb + sigma)";
+    else if (m.n[m.num_layers - 1] > 32) w = "fused path needs a head with <= 32 outputs";
     else {
         for (int l = 0; l < m.num_layers && !w; ++l) {
             if (m.k[l] < 1 || m.k[l] > kNT * 32 || m.n[l] < 1 || m.n[l] > kNT * 32)
@@ -888,6 +968,15 @@ static FusedArgs make_fused_args(const FusedPlan& p, const lnerf_batch& b, float
     return a;
 }
 
+static void launch_fused(const FusedPlan& p, const FusedArgs& fa, hipStream_t s) {
+    int ht = 1;
+    for (int l = 0; l + 1 < p.L; ++l) ht = p.nt[l] > ht ? p.nt[l] : ht;
+    if (ht <= 1) fused_fwd_bwd_kernel<1><<<p.num_wg, kWgThreads, 0, s>>>(fa);
+    else if (ht <= 2) fused_fwd_bwd_kernel<2><<<p.num_wg, kWgThreads, 0, s>>>(fa);
+    else if (ht <= 4) fused_fwd_bwd_kernel<4><<<p.num_wg, kWgThreads, 0, s>>>(fa);
+    else fused_fwd_bwd_kernel<8><<<p.num_wg, kWgThreads, 0, s>>>(fa);
+}
+
 void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, const lnerf_batch& b,
                       float seed, int flags, const lnerf_outputs& out, hipStream_t s,
                       hipEvent_t* ev) {
@@ -899,7 +988,7 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
     launch_pack(p, ws, bs, s);
     mark(1);
     FusedArgs fa = make_fused_args(p, b, seed_loss ? 1.0f : seed, out, true);
-    fused_fwd_bwd_kernel<<<p.num_wg, kWgThreads, 0, s>>>(fa);
+    launch_fused(p, fa, s);
     mark(2);
     loss_reduce_kernel<<<1, 64, 0, s>>>(p.loss_part, p.num_wg, p.loss_total, out.loss);
     mark(3);
@@ -920,6 +1009,10 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
     da.blocks = p.blocks;
     da.dw_part = p.dw_part;
     da.db_part = p.db_part;
+    {
+        const char* e = getenv("LNERF_DW_MODE");
+        da.dbg = e ? atoi(e) : 0;
+    }
     dw_kernel<<<p.dw_grid, kWgThreads, 0, s>>>(da);
     mark(4);
     ReduceArgs ra{};
@@ -929,9 +1022,7 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
         ra.n[l] = p.n[l];
         ra.kt[l] = p.kt[l];
         ra.nt[l] = p.nt[l];
-        const int nblk = ((p.kt[l] + 3) / 4) * ((p.nt[l] + 3) / 4);
-        const int P = nblk >= kWaves ? 1 : kWaves / nblk;
-        ra.nparts[l] = p.dw_splits[l] * P;
+        ra.nparts[l] = p.dw_splits[l];
         ra.splits[l] = p.dw_splits[l];
         ra.dwp_off[l] = p.dwp_off[l];
         ra.dbp_off[l] = p.dbp_off[l];
@@ -958,7 +1049,7 @@ void fused_render(const FusedPlan& p, const float* ws, const float* bs, const ln
                   const lnerf_outputs& out, hipStream_t s) {
     launch_pack(p, ws, bs, s);
     FusedArgs fa = make_fused_args(p, b, 1.0f, out, false);
-    fused_fwd_bwd_kernel<<<p.num_wg, kWgThreads, 0, s>>>(fa);
+    launch_fused(p, fa, s);
     loss_reduce_kernel<<<1, 64, 0, s>>>(p.loss_part, p.num_wg, p.loss_total, out.loss);
 }
 

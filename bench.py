@@ -79,6 +79,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import numpy as np
     import torch
+    import dp
     import lnerf
     import scene
 
@@ -111,8 +112,8 @@ def main():
         else:
             eng.train_step(mlp, ws, bs, pts, dists, target, samples=S, num_freqs=b["F"],
                            seed=1.0, flags=f, grads=grads, acc_color=acc)
-            dist.all_reduce(gbuf)                      # [dW, db, loss] SUM over ranks (RCCL)
-            eng.scale_by_device_scalar(gbuf[:-1], gbuf[-1:])
+            # [dW, db, loss] SUM over ranks (RCCL), then the loss seed (loma-nerf_amd/dp.py)
+            dp.allreduce_loss_seeded(gbuf, dist, eng.scale_by_device_scalar)
 
     for _ in range(args.warmup):
         step()

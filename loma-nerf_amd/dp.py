@@ -1,0 +1,31 @@
+"""Data-parallel step glue: one process per GPU, rays sharded, one RCCL all-reduce per step.
+
+The loss is a sum over rays (scripts/nerf.py:297-302) and the reference seeds its gradient with
+that loss (train_nerf.py:477). Each rank therefore computes *unit-seeded* gradients of its own rays
+into a packed buffer [dW (L*w_k*w_n) | db (L*w_n) | loss (1)]; one SUM all-reduce (RCCL over xGMI
+with the "nccl" backend, gloo on CPU) yields the global unit-seeded gradients and the global
+loss; multiplying the gradient part by the reduced loss gives exactly the loss-seeded gradient of
+the whole batch. The optimizer update is then replicated, so weights stay identical on all ranks.
+"""
+from __future__ import annotations
+
+
+def shard_rays(n_rays: int, world: int, rank: int):
+    """Contiguous ray range of `rank` (SURVEY.md §8e partitioning)."""
+    lo = n_rays * rank // world
+    hi = n_rays * (rank + 1) // world
+    return lo, hi
+
+
+def allreduce_loss_seeded(packed, dist, scale_fn=None, group=None):
+    """SUM-all-reduce the packed [grads | loss] buffer, then scale grads by the global loss.
+
+    `scale_fn(buf, scalar)` does buf *= scalar on the buffer's device (the engine's
+    lnerf_scale_by_device_scalar on GPU); defaults to an in-place tensor multiply."""
+    dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
+    grads, loss = packed[:-1], packed[-1:]
+    if scale_fn is None:
+        grads.mul_(loss)
+    else:
+        scale_fn(grads, loss)
+    return packed

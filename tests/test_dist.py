@@ -1,0 +1,87 @@
+"""Multi-process (world_size 2, gloo, CPU) test of the data-parallel protocol in
+loma-nerf_amd/dp.py: each rank computes unit-seeded gradients of its ray shard (here with the C
+oracle standing in for the device kernels), one SUM all-reduce of the packed [dW | db | loss]
+buffer, then scaling by the reduced loss must equal the loss-seeded gradient of the full batch
+(train_nerf.py:477 seeds the gradient with the loss; the loss is a sum over rays)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    for p in (os.path.join(repo, "oracle"), os.path.join(repo, "loma-nerf_amd")):
+        sys.path.insert(0, p)
+    import dp
+    import nerf_np
+    import oracle
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    w = nerf_np.make_workload("cfg2", rays=20, samples=8)
+    shapes = [x.shape for x in w.ws]
+    lo, hi = dp.shard_rays(w.N, world, rank)
+    X = w.X.reshape(w.N, w.S, -1)[lo:hi].reshape(-1, w.X.shape[1])
+    r = oracle.standard_forward_backward(X, w.wp, w.bp, shapes, w.dists[lo:hi], w.target[lo:hi],
+                                         w.S, seed=1.0)
+    packed = torch.from_numpy(np.concatenate([r["dW"].ravel(), r["dB"].ravel(),
+                                              [np.float32(r["loss"])]]).astype(np.float32))
+    dp.allreduce_loss_seeded(packed, dist)
+    if rank == 0:
+        out.put(packed.numpy().copy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_allreduce_matches_full_batch(oracle_lib):
+    import nerf_np
+    import oracle
+    from loma_calls import assert_close
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    w = nerf_np.make_workload("cfg2", rays=20, samples=8)
+    shapes = [x.shape for x in w.ws]
+    full = oracle.standard_forward_backward(w.X, w.wp, w.bp, shapes, w.dists, w.target, w.S,
+                                            seed=None)
+    nW = full["dW"].size
+    nB = full["dB"].size
+    assert abs(got[-1] - full["loss"]) <= 1e-5 * full["loss"]
+    assert_close("dW", got[:nW].reshape(full["dW"].shape), full["dW"], rtol=1e-4, atol_scale=1e-5)
+    assert_close("dB", got[nW:nW + nB].reshape(full["dB"].shape), full["dB"], rtol=1e-4,
+                 atol_scale=1e-5)
+
+
+def test_shard_rays_partitions():
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "loma-nerf_amd"))
+    import dp
+    for n in (1, 7, 4096):
+        for world in (1, 2, 3, 8):
+            spans = [dp.shard_rays(n, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            for (a, b), (c, d) in zip(spans, spans[1:]):
+                assert b == c

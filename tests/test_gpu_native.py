@@ -166,3 +166,74 @@ def test_full_size_oracle_rays_spotcheck(engine, full):
     assert_close("acc", g["acc"][idx], want["acc"], **TOL)
     assert_close("d_target", g["d_target"][idx], want["d_target"], **TOL)
     assert_close("d_dists", g["d_dists"][idx], want["d_dists"], **TOL)
+
+
+# ---- against the committed golden fixtures (float64 numpy restatement) ------------------------
+
+@pytest.mark.parametrize("name", ["chunk_4x30.npz", "deep8_w64_2x64.npz", "trained_weights_8x16.npz"])
+def test_fused_matches_golden_fixture(engine, name):
+    import os
+    import lnerf
+    import torch
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", name)
+    g = dict(np.load(path, allow_pickle=False))
+    shapes = [tuple(int(v) for v in s) for s in g["shapes"]]
+    S = int(g["S"])
+    mlp = lnerf.make_mlp(shapes, g["wp"].shape[1], g["wp"].shape[2])
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to("cuda:0")
+    r = engine.train_step(mlp, d(g["wp"]), d(g["bp"]), d(g["X"]), d(g["dists"]), d(g["target"]),
+                          samples=S, input_mode=lnerf.INPUT_ENCODED, seed=1.0, want_per_ray=True,
+                          want_dx=True, flags=lnerf.FAST)
+    torch.cuda.synchronize()
+    assert abs(float(r.loss.item()) - g["loss"]) <= 1e-5 * abs(g["loss"])
+    assert_close("acc", r.acc_color.cpu().numpy(), g["acc"], **TOL)
+    assert_close("dW", r.d_ws.cpu().numpy(), g["dW"], **TOL)
+    assert_close("dB", r.d_bs.cpu().numpy(), g["dB"], **TOL)
+    assert_close("dX", r.d_x.cpu().numpy(), g["dX"], **TOL)
+    assert_close("d_dists", r.d_dists.cpu().numpy(), g["d_dists"], **TOL)
+    assert_close("d_target", r.d_target.cpu().numpy(), g["d_target"], **TOL)
+
+
+def test_single_hip_runtime_mapped(engine):
+    """torch and libloma_nerf.so must share one libamdhip64 (one HIP runtime per process)."""
+    maps = open("/proc/self/maps").read().splitlines()
+    libs = sorted(set(l.split()[-1] for l in maps if "libamdhip64" in l))
+    real = sorted(set(__import__("os").path.realpath(p) for p in libs))
+    assert len(real) == 1, libs
+    assert any("libloma_nerf.so" in l for l in maps)
+
+
+def test_render_forward_only_matches_train_forward(engine):
+    """lnerf_render (eval path, train_nerf.py:616-661) gives the training forward's colours."""
+    import lnerf
+    import torch
+    w = nerf_np.make_workload("cfg2", rays=300)
+    shapes = [x.shape for x in w.ws]
+    mlp = lnerf.make_mlp(shapes, w.wp.shape[1], w.wp.shape[2])
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to("cuda:0")
+    loss, acc = engine.render(mlp, d(w.wp), d(w.bp), d(w.pts32.reshape(-1, 3)), d(w.dists),
+                              d(w.target), samples=w.S, num_freqs=w.F)
+    tr = run_native(engine, w, seed=1.0)
+    torch.cuda.synchronize()
+    assert np.array_equal(acc.cpu().numpy(), tr["acc"])
+    assert float(loss.item()) == tr["loss"]
+
+
+def test_adam_matches_reference_update(engine):
+    """lnerf_adam_update vs train_nerf.py:143-161 (numpy, float32 arrays)."""
+    import torch
+    rng = np.random.RandomState(0)
+    p = rng.standard_normal(1000).astype(np.float32)
+    g = rng.standard_normal(1000).astype(np.float32)
+    m = np.zeros_like(p)
+    v = np.zeros_like(p)
+    lr, b1, b2, eps = 5e-4, 0.9, 0.999, 1e-8
+    pd, gd, md, vd = (torch.from_numpy(x.copy()).to("cuda:0") for x in (p, g, m, v))
+    for t in (1, 2, 3):
+        lr_t = lr * (np.sqrt(1 - b2 ** t) / (1 - b1 ** t))
+        m = b1 * m + (1 - b1) * g
+        v = b2 * v + (1 - b2) * (g ** 2)
+        p = p - lr_t * (m / (1 - b1 ** t)) / (np.sqrt(v / (1 - b2 ** t)) + eps)
+        engine.adam_update(pd, gd, md, vd, t, lr, b1, b2, eps)
+    torch.cuda.synchronize()
+    assert np.allclose(pd.cpu().numpy(), p, rtol=1e-5, atol=1e-7)

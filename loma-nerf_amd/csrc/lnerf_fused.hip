@@ -124,11 +124,14 @@ __device__ __forceinline__ void store_tile(const fx16& v, float* __restrict__ ds
 // While chunk c computes, input tile c-1 (already consumed) is written to its HBM slab
 // (`tstore`, nullable), so the slab stores drain under the MFMAs instead of stalling a barrier.
 // `bias_src` (nullable) = this layer's fragment-ordered biases, staged into `bias_lds`.
-template <int NTO>
+// NCH > 0: compile-time chunk count (no per-chunk branch around the MFMAs: such a branch makes
+// the compiler copy the accumulators between AGPRs and VGPRs); NCH = 0: runtime `nchunks`.
+template <int NTO, int NCH = 0>
 __device__ __forceinline__ void mma_stream_t(const float* __restrict__ src, int nchunks,
                                              const fx16 (&in)[kNT], fx16 (&out)[kNT], float* ldsw,
                                              float* tstore, float* tr, const float* bias_src,
                                              float* bias_lds) {
+    if (NCH > 0) nchunks = NCH;
     const int lane = threadIdx.x & 63;
     constexpr int NT4 = (NTO + 3) / 4;
     constexpr int CF = 16 * NT4 * 256;
@@ -138,8 +141,8 @@ __device__ __forceinline__ void mma_stream_t(const float* __restrict__ src, int 
                                          (__attribute__((address_space(3))) void*)bias_lds, 16, 0, 0);
     dma_barrier();
 #pragma unroll
-    for (int c = 0; c < kNT; ++c) {
-        if (c < nchunks) {
+    for (int c = 0; c < (NCH > 0 ? NCH : kNT); ++c) {
+        if (NCH > 0 || c < nchunks) {
             if (tstore && c >= 1) store_tile(in[c - 1], tstore + (c - 1) * 1024, tr);
             const float* cur = ldsw + (c & 1) * kChunkMax + lane * 4;
             if (c + 1 < nchunks)
@@ -351,6 +354,7 @@ __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs 
                         : (l == 0 ? a.act + a.x_off + blk * (size_t)(a.kt[0] * 1024)
                                   : a.act + a.act_off[l - 1] + blk * (size_t)(a.kt[l] * 1024));
         float* bl = biasl + (l & 1) * (kNT * 32);
+        // hidden layers l >= 1 and the head contract over HT tiles (k_l = n_{l-1})
         if (l < a.L - 1) mma_stream_t<HT>(a.wf + a.wf_off[l], a.kt[l], act, out, ldsw, ts, tr, a.bp + a.bp_off[l], bl);
         else mma_stream_t<1>(a.wf + a.wf_off[l], a.kt[l], act, out, ldsw, ts, tr, a.bp + a.bp_off[l], bl);
         if (l < a.L - 1) {
@@ -494,12 +498,14 @@ struct DwArgs {
     size_t g_off[kMaxLayers];
     int blocks;
     int splits[kMaxLayers];
-    int wg_off[kMaxLayers];     // first workgroup of layer l
+    int nl;                     // layers in this launch
+    int lid[kMaxLayers];        // their layer ids
+    int wg_off[kMaxLayers + 1]; // first workgroup of the i-th layer of this launch
     float* dw_part;
     size_t dwp_off[kMaxLayers];
     float* db_part;
     size_t dbp_off[kMaxLayers];
-    int dbg;  // ablation (LNERF_DW_MODE): 0 normal, 1 loads only, 2 compute only
+    int mode[kMaxLayers];       // 0: 4x4-tile blocks per wave; >0: phased (see dw_kernel)
 };
 
 __device__ __forceinline__ int swz_chunk(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
@@ -524,14 +530,14 @@ __device__ __forceinline__ fx4 dw_frag(const float* base, int row, int g, int h)
     return *(const fx4*)(base + row * 32 + c * 4);
 }
 
-// One wave's TI x TJ block of 32x32 output tiles over one staged slab pair. Sample order inside
-// the contraction: step (g, u) pairs lane half h with sample 8g + 4h + u (same for A and G).
+// One wave's TI x TJ tiles over sample steps g in [g0, g1) of a staged slab pair (a g-step = 8
+// samples: lane half h takes samples 8g + 4h + u, u = 0..3, for A and G alike).
 template <int TI, int TJ>
-__device__ __forceinline__ void dw_block(const float* ca, const float* cg, int kb, int jb,
-                                         fx16 (&acc)[4][4]) {
+__device__ __forceinline__ void dw_block(const float* ca, const float* cg, int kb, int jb, int g0,
+                                         int g1, fx16 (&acc)[TI][TJ]) {
     const int lane = threadIdx.x & 63, h = lane >> 5, rl = lane & 31;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = g0; g < g1; ++g) {
         fx4 af[TI], bf[TJ];
 #pragma unroll
         for (int i = 0; i < TI; ++i) af[i] = dw_frag(ca, (kb + i) * 32 + rl, g, h);
@@ -547,50 +553,41 @@ __device__ __forceinline__ void dw_block(const float* ca, const float* cg, int k
     }
 }
 
-__device__ __forceinline__ void dw_block_dispatch(int ti, int tj, const float* ca, const float* cg,
-                                                  int kb, int jb, fx16 (&acc)[4][4]) {
-    switch (ti * 4 + tj) {
-#define LNERF_DWB(I, J) \
-    case I * 4 + J: dw_block<I, J>(ca, cg, kb, jb, acc); break;
-        LNERF_DWB(1, 1) LNERF_DWB(1, 2) LNERF_DWB(1, 3) LNERF_DWB(1, 4)
-        LNERF_DWB(2, 1) LNERF_DWB(2, 2) LNERF_DWB(2, 3) LNERF_DWB(2, 4)
-        LNERF_DWB(3, 1) LNERF_DWB(3, 2) LNERF_DWB(3, 3) LNERF_DWB(3, 4)
-        LNERF_DWB(4, 1) LNERF_DWB(4, 2) LNERF_DWB(4, 3) LNERF_DWB(4, 4)
-#undef LNERF_DWB
-        default: break;
-    }
-}
-
-__global__ void __launch_bounds__(kWgThreads, 1) dw_kernel(DwArgs a) {
-    __shared__ __attribute__((aligned(16))) float lds[2 * kDwStageFloats];
+// The whole per-workgroup pass for one layer. PHASED = false: wave w owns a 4x4 block of the
+// layer's output tiles and every sample; PHASED = true (small layers, TI*TJ <= 16 tiles): every
+// wave owns all TI x TJ tiles and one of the 4 sample steps of each slab, writing its own
+// partial (4 partials per split). Each instantiation keeps its accumulators to itself.
+template <int TI, int TJ, bool PHASED>
+__device__ __forceinline__ void dw_run(const DwArgs a, int l, int sp, float* lds) {
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // which layer / split (uniform)
-    int l = 0;
-    while (l + 1 < a.L && (int)blockIdx.x >= a.wg_off[l + 1]) ++l;
-    const int sp = blockIdx.x - a.wg_off[l];
     const int KT = a.kt[l], NTo = a.nt[l];
-    const int nbj = (NTo + 3) >> 2, nblk = ((KT + 3) >> 2) * nbj;
-    const bool active = wave < nblk;
-    // idle waves (layers with < 4 tile blocks) repeat block 0 unconditionally and discard it:
-    // a branch around the MFMAs would make the compiler shuttle the accumulators out of AGPRs
-    const int kb = active ? (wave / nbj) * 4 : 0, jb = active ? (wave % nbj) * 4 : 0;
-    const int ti = min(4, KT - kb), tj = min(4, NTo - jb);
+    int kb = 0, jb = 0, ti = TI, tj = TJ;
+    bool active = true;
+    if (!PHASED) {
+        const int nbj = (NTo + 3) >> 2, nblk = ((KT + 3) >> 2) * nbj;
+        active = wave < nblk;
+        // idle waves repeat block 0 unconditionally and discard it (a branch around the MFMAs
+        // would make the compiler shuttle the accumulators out of AGPRs)
+        kb = active ? (wave / nbj) * 4 : 0;
+        jb = active ? (wave % nbj) * 4 : 0;
+        ti = min(TI, KT - kb);
+        tj = min(TJ, NTo - jb);
+    }
+    const int g0 = PHASED ? wave : 0, g1 = PHASED ? wave + 1 : 4;
     const int splits = a.splits[l];
     const int per = (a.blocks + splits - 1) / splits;
     const int b0 = min(a.blocks, sp * per), b1 = min(a.blocks, b0 + per);
     const int a_rows = KT * 32, g_rows = NTo * 32;
     const float* A = a.act + a.a_off[l];
     const float* G = a.grad + a.g_off[l];
-
-    fx16 acc[4][4];
+    fx16 acc[TI][TJ];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (int j = 0; j < TJ; ++j) acc[i][j] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     float dbsum = 0.0f;
 
-    const bool do_load = a.dbg != 2, do_mma = a.dbg != 1;
     if (b0 < b1) {
         dw_stage(A + (size_t)b0 * a_rows * 32, lds, a_rows, wave, lane);
         dw_stage(G + (size_t)b0 * g_rows * 32, lds + kDwRows * 32, g_rows, wave, lane);
@@ -598,15 +595,16 @@ __global__ void __launch_bounds__(kWgThreads, 1) dw_kernel(DwArgs a) {
     dma_barrier();
     for (int b = b0; b < b1; ++b) {
         float* cur = lds + ((b - b0) & 1) * kDwStageFloats;
-        if (b + 1 < b1 && do_load) {
+        if (b + 1 < b1) {
             float* nxt = lds + ((b + 1 - b0) & 1) * kDwStageFloats;
             dw_stage(A + (size_t)(b + 1) * a_rows * 32, nxt, a_rows, wave, lane);
             dw_stage(G + (size_t)(b + 1) * g_rows * 32, nxt + kDwRows * 32, g_rows, wave, lane);
         }
         const float* ca = cur;
         const float* cg = cur + kDwRows * 32;
-        // full 4x4 blocks: rows past the staged slab read stale LDS, those tiles are never written
-        if (do_mma) dw_block<4, 4>(ca, cg, kb, jb, acc);
+        // (unconditional: a branch around the MFMAs makes the compiler shuttle the accumulators
+        // between AGPRs and VGPRs every slab)
+        dw_block<TI, TJ>(ca, cg, kb, jb, g0, g1, acc);
         if (tid < g_rows) {
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
@@ -616,14 +614,15 @@ __global__ void __launch_bounds__(kWgThreads, 1) dw_kernel(DwArgs a) {
         }
         dma_barrier();
     }
-    // partial slab: [split][k][j], k < KT*32, j < NTo*32
+    // partial slab: [split * P + phase][k][j], k < KT*32, j < NTo*32
     if (active) {
         const int ncol = NTo * 32;
-        float* part = a.dw_part + a.dwp_off[l] + (size_t)sp * (KT * 32) * ncol;
+        const int part_id = PHASED ? sp * kWaves + wave : sp;
+        float* part = a.dw_part + a.dwp_off[l] + (size_t)part_id * (KT * 32) * ncol;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < TJ; ++j)
                 if (i < ti && j < tj) {
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
@@ -634,6 +633,39 @@ __global__ void __launch_bounds__(kWgThreads, 1) dw_kernel(DwArgs a) {
                 }
     }
     if (tid < g_rows) a.db_part[a.dbp_off[l] + (size_t)sp * g_rows + tid] = dbsum;
+}
+
+// Phased shapes (KT x NTo tiles) with their own instantiation; anything else runs the blocked
+// 4x4 path. Mode ids must match dw_mode_for() on the host.
+#define LNERF_DW_PHASED_SHAPES(X) X(1, 1, 1) X(2, 1, 2) X(1, 2, 3) X(2, 2, 4) X(2, 4, 5) X(4, 2, 6) \
+    X(2, 8, 7) X(8, 1, 8) X(4, 1, 9) X(1, 4, 10) X(8, 2, 11) X(1, 8, 12) X(4, 4, 13)
+
+// One launch per group of layers sharing an instantiation (all blocked layers together, each
+// phased shape on its own), so no kernel merges different accumulator sets.
+template <int TI, int TJ, bool PHASED>
+__global__ void __launch_bounds__(kWgThreads, 1) dw_kernel(DwArgs a) {
+    __shared__ __attribute__((aligned(16))) float lds[2 * kDwStageFloats];
+    int i = 0;
+    while (i + 1 < a.nl && (int)blockIdx.x >= a.wg_off[i + 1]) ++i;
+    dw_run<TI, TJ, PHASED>(a, a.lid[i], blockIdx.x - a.wg_off[i], lds);
+}
+
+void launch_dw(int mode, int grid, const DwArgs& a, hipStream_t s) {
+    switch (mode) {
+#define LNERF_DW_CASE(I, J, M) \
+    case M: dw_kernel<I, J, true><<<grid, kWgThreads, 0, s>>>(a); break;
+        LNERF_DW_PHASED_SHAPES(LNERF_DW_CASE)
+#undef LNERF_DW_CASE
+        default: dw_kernel<4, 4, false><<<grid, kWgThreads, 0, s>>>(a); break;
+    }
+}
+
+int dw_mode_for(int kt, int nt) {
+#define LNERF_DW_MODE_OF(I, J, M) \
+    if (kt == I && nt == J) return M;
+    LNERF_DW_PHASED_SHAPES(LNERF_DW_MODE_OF)
+#undef LNERF_DW_MODE_OF
+    return 0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -694,13 +726,24 @@ __global__ void pack_kernel(PackArgs a, int l) {
 // ---------------------------------------------------------------------------------------------
 // reductions
 // ---------------------------------------------------------------------------------------------
-__global__ void loss_reduce_kernel(const float* __restrict__ part, int n, float* total,
-                                   float* out_loss) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// Deterministic two-level sum of the per-workgroup partial losses: 256 strided sequential
+// sums, then a fixed-order tree in LDS.
+__global__ void __launch_bounds__(256) loss_reduce_kernel(const float* __restrict__ part, int n,
+                                                          float* total, float* out_loss) {
+    __shared__ float red[256];
+    const int t = threadIdx.x;
     float s = 0.0f;
-    for (int i = 0; i < n; ++i) s = s + part[i];
-    *total = s;
-    if (out_loss) *out_loss = s;
+    for (int i = t; i < n; i += 256) s += part[i];
+    red[t] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (t < w) red[t] = red[t] + red[t + w];
+        __syncthreads();
+    }
+    if (t == 0) {
+        *total = red[0];
+        if (out_loss) *out_loss = red[0];
+    }
 }
 
 struct ReduceArgs {
@@ -763,7 +806,7 @@ struct Layout {
     size_t pack_total;
     size_t act_off[kMaxLayers], x_off, act_total;
     size_t grad_off[kMaxLayers], grad_total;
-    int splits[kMaxLayers], phases[kMaxLayers], wg_off[kMaxLayers], dw_grid;
+    int splits[kMaxLayers], phases[kMaxLayers], mode[kMaxLayers], wg_off[kMaxLayers], dw_grid;
     size_t dwp_off[kMaxLayers], dwp_total, dbp_off[kMaxLayers], dbp_total;
     int num_wg, blocks, rpw;
 };
@@ -795,17 +838,22 @@ void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S) {
     off = 0;
     for (int l = 0; l < L; ++l) { y.grad_off[l] = off; off += (size_t)y.blocks * nt[l] * 1024; }
     y.grad_total = off;
-    // dW grid: every workgroup runs full 4x4-tile wave blocks over its slabs, so a workgroup's time
-    // is set by its slab count alone -> give every layer the same split count, one wave of
-    // workgroups over the 256 CUs (1 workgroup per CU: 128 KiB of LDS).
-    int wg = 0;
+    // dW launches: one per instantiation group (blocked layers together; each phased small-layer
+    // shape alone). A blocked group spreads ~256 workgroups over its layers (1 per CU: 128 KiB
+    // of LDS); a phased layer costs ~1/4..1/16 of a blocked one per slab and gets 128.
     size_t dwp = 0, dbp = 0;
+    int nblocked = 0;
     for (int l = 0; l < L; ++l) {
-        int sp = 256 / L;
+        y.mode[l] = dw_mode_for(kt[l], nt[l]);
+        if (!y.mode[l]) ++nblocked;
+    }
+    int wg = 0;
+    for (int l = 0; l < L; ++l) {
+        int sp = y.mode[l] ? 128 : 256 / (nblocked ? nblocked : 1);
         sp = sp < 1 ? 1 : sp;
         sp = sp > y.blocks ? y.blocks : sp;
         y.splits[l] = sp;
-        y.phases[l] = 1;
+        y.phases[l] = y.mode[l] ? kWaves : 1;
         y.wg_off[l] = wg;
         wg += sp;
         y.dwp_off[l] = dwp;
@@ -864,6 +912,8 @@ void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws
         p.act_off[l] = (l < p.L - 1) ? y.act_off[l] : 0;
         p.grad_off[l] = y.grad_off[l];
         p.dw_splits[l] = y.splits[l];
+        p.dw_mode[l] = y.mode[l];
+        p.dw_phases[l] = y.phases[l];
         p.dw_split_off[l] = y.wg_off[l];
         p.dwp_off[l] = y.dwp_off[l];
         p.dbp_off[l] = y.dbp_off[l];
@@ -990,7 +1040,7 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
     FusedArgs fa = make_fused_args(p, b, seed_loss ? 1.0f : seed, out, true);
     launch_fused(p, fa, s);
     mark(2);
-    loss_reduce_kernel<<<1, 64, 0, s>>>(p.loss_part, p.num_wg, p.loss_total, out.loss);
+    loss_reduce_kernel<<<1, 256, 0, s>>>(p.loss_part, p.num_wg, p.loss_total, out.loss);
     mark(3);
     DwArgs da{};
     da.L = p.L;
@@ -1000,7 +1050,7 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
         da.a_off[l] = (l == 0) ? p.act_off[kMaxLayers - 1] : p.act_off[l - 1];
         da.g_off[l] = p.grad_off[l];
         da.splits[l] = p.dw_splits[l];
-        da.wg_off[l] = p.dw_split_off[l];
+        da.mode[l] = p.dw_mode[l];
         da.dwp_off[l] = p.dwp_off[l];
         da.dbp_off[l] = p.dbp_off[l];
     }
@@ -1009,11 +1059,24 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
     da.blocks = p.blocks;
     da.dw_part = p.dw_part;
     da.db_part = p.db_part;
-    {
-        const char* e = getenv("LNERF_DW_MODE");
-        da.dbg = e ? atoi(e) : 0;
+    // one launch per instantiation group
+    bool done[kMaxLayers] = {};
+    for (int l0 = 0; l0 < p.L; ++l0) {
+        if (done[l0]) continue;
+        const int mode = p.dw_mode[l0];
+        da.nl = 0;
+        int grid = 0;
+        for (int l = l0; l < p.L; ++l) {
+            if (done[l] || p.dw_mode[l] != mode) continue;
+            done[l] = true;
+            da.lid[da.nl] = l;
+            da.wg_off[da.nl] = grid;
+            grid += p.dw_splits[l];
+            ++da.nl;
+        }
+        da.wg_off[da.nl] = grid;
+        launch_dw(mode, grid, da, s);
     }
-    dw_kernel<<<p.dw_grid, kWgThreads, 0, s>>>(da);
     mark(4);
     ReduceArgs ra{};
     ra.L = p.L;
@@ -1022,7 +1085,7 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
         ra.n[l] = p.n[l];
         ra.kt[l] = p.kt[l];
         ra.nt[l] = p.nt[l];
-        ra.nparts[l] = p.dw_splits[l];
+        ra.nparts[l] = p.dw_splits[l] * p.dw_phases[l];
         ra.splits[l] = p.dw_splits[l];
         ra.dwp_off[l] = p.dwp_off[l];
         ra.dbp_off[l] = p.dbp_off[l];
@@ -1050,7 +1113,7 @@ void fused_render(const FusedPlan& p, const float* ws, const float* bs, const ln
     launch_pack(p, ws, bs, s);
     FusedArgs fa = make_fused_args(p, b, 1.0f, out, false);
     launch_fused(p, fa, s);
-    loss_reduce_kernel<<<1, 64, 0, s>>>(p.loss_part, p.num_wg, p.loss_total, out.loss);
+    loss_reduce_kernel<<<1, 256, 0, s>>>(p.loss_part, p.num_wg, p.loss_total, out.loss);
 }
 
 }  // namespace lnerf

@@ -110,6 +110,8 @@ struct FusedPlan {
     float* dw_part;   // dW split partials
     float* db_part;   // dB split partials
     int dw_splits[kMaxLayers];
+    int dw_mode[kMaxLayers];       // dW kernel instantiation per layer (0 = blocked 4x4)
+    int dw_phases[kMaxLayers];     // partials per split (4 for phased small layers)
     int dw_split_off[kMaxLayers];  // workgroup offset of layer l in the dW grid
     size_t dwp_off[kMaxLayers];    // float offset of layer l's partial slabs in dw_part
     size_t dbp_off[kMaxLayers];

@@ -42,6 +42,24 @@ def parse():
     return ap.parse_args()
 
 
+def pmc_traffic(kernel, config):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
+    (profiles/<round>_pmc.json, written by scripts/summarize_profile.py from separate FETCH_SIZE /
+    WRITE_SIZE passes of this same command, gfx950-corrected), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", "r*_pmc.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    if d.get("workload") != config:
+        return None
+    for name, v in d["kernels"].items():
+        if name.startswith(kernel):
+            return {"bytes": v["hbm_bytes_per_launch"], "read": v["hbm_read_bytes"],
+                    "write": v["hbm_write_bytes"], "source": os.path.relpath(files[-1], HERE)}
+    return None
+
+
 def cpu_baseline(args, cfg):
     """The C oracle (loma-order scalar fp32 restatement, -O2, no FMA) timed on this host on a
     bounded sample of the same workload. Test infrastructure, used only as the reported baseline."""
@@ -51,7 +69,6 @@ def cpu_baseline(args, cfg):
     import scene
     b = scene.make_batch(cfg, rays=args.cpu_rays)
     shapes, wp, bp = scene.init_mlp(3 + 6 * b["F"], 4, b["L"], b["H"])
-    X = oracle.positional_encoding_3d(b["pts"].astype(np.float64), b["F"])
     res = {}
     for threads, rays in ((1, args.cpu_rays), (args.cpu_threads, args.cpu_rays * args.cpu_threads)):
         bb = scene.make_batch(cfg, rays=rays)
@@ -62,7 +79,6 @@ def cpu_baseline(args, cfg):
         oracle.train_step(Xb, wp, bp, shapes, bb["dists"], bb["target"], bb["S"], threads=threads)
         dt = time.perf_counter() - t0
         res[threads] = (rays * bb["S"] / dt, rays, dt)
-    del X
     v1, r1, t1 = res[1]
     vn, rn, tn = res[args.cpu_threads]
     return ({"value": v1, "unit": "ray-samples/s", "cores": 1, "kind": "port",
@@ -85,7 +101,9 @@ def main():
 
     torch.cuda.set_device(local)
     dist = None
-    if world > 1:
+    # under torchrun (WORLD_SIZE set) the RCCL data-parallel step runs even at world size 1, so the
+    # N>1 code path can be rehearsed on a single GPU
+    if world > 1 or "WORLD_SIZE" in os.environ:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     dev = f"cuda:{local}"
@@ -106,7 +124,7 @@ def main():
 
     def step(timing=False):
         f = flags | (lnerf.TIMING if timing else 0)
-        if world == 1:
+        if dist is None:
             eng.train_step(mlp, ws, bs, pts, dists, target, samples=S, num_freqs=b["F"],
                            seed=None, flags=f, grads=grads, acc_color=acc)
         else:
@@ -170,6 +188,12 @@ def main():
                                "frac": fused_flops / (fus_ms / 1e3) / 1e12 / PEAK_FP32_TFLOPS,
                                "traffic": None,
                                "flops_per_launch": fused_flops, "avg_ms": fus_ms}
+            tr = pmc_traffic("fused_fwd_bwd_kernel", args.config) if args.rays is None else None
+            if tr:
+                out["roofline"]["traffic"] = tr["bytes"]
+                out["roofline"]["traffic_unit"] = "bytes/launch"
+                out["roofline"]["traffic_source"] = tr["source"]
+                out["roofline"]["traffic_gbs"] = tr["bytes"] / (fus_ms / 1e3) / 1e9
             out["kernels_ms"] = kt
             out["dw_kernel_tflops"] = dw_flops / (kt["dw"] / 1e3) / 1e12
         if world == 1 and not args.no_cpu_baseline:

@@ -124,8 +124,9 @@ __device__ __forceinline__ void store_tile(const fx16& v, float* __restrict__ ds
 // While chunk c computes, input tile c-1 (already consumed) is written to its HBM slab
 // (`tstore`, nullable), so the slab stores drain under the MFMAs instead of stalling a barrier.
 // `bias_src` (nullable) = this layer's fragment-ordered biases, staged into `bias_lds`.
-// NCH > 0: compile-time chunk count (no per-chunk branch around the MFMAs: such a branch makes
-// the compiler copy the accumulators between AGPRs and VGPRs); NCH = 0: runtime `nchunks`.
+// NCH > 0: compile-time chunk count (drops the per-chunk branch, which makes the compiler copy
+// accumulators between AGPRs and VGPRs); NCH = 0: runtime `nchunks`. The call sites use NCH = 0:
+// with NCH = HT = 8 the scheduler hoists the next chunks' LDS reads and the kernel spills.
 template <int NTO, int NCH = 0>
 __device__ __forceinline__ void mma_stream_t(const float* __restrict__ src, int nchunks,
                                              const fx16 (&in)[kNT], fx16 (&out)[kNT], float* ldsw,
@@ -762,6 +763,22 @@ struct ReduceArgs {
     int accumulate;
 };
 
+// In-order sum of n strided partials (deterministic); loads are issued 8 at a time so the
+// reduction streams at HBM rate instead of waiting on one load per add.
+__device__ __forceinline__ float sum_parts(const float* __restrict__ p, size_t stride, int n) {
+    float s = 0.0f;
+    int q = 0;
+    for (; q + 8 <= n; q += 8) {
+        float t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = __builtin_nontemporal_load(p + (size_t)(q + u) * stride);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += t[u];
+    }
+    for (; q < n; ++q) s += p[(size_t)q * stride];
+    return s;
+}
+
 __global__ void grad_reduce_kernel(ReduceArgs a) {
     const size_t nW = (size_t)a.L * a.w_k * a.w_n, nB = (size_t)a.L * a.w_n;
     const float sc = a.scale ? *a.scale : 1.0f;
@@ -776,9 +793,8 @@ __global__ void grad_reduce_kernel(ReduceArgs a) {
                 const int ncol = a.nt[l] * 32;
                 const size_t slab = (size_t)a.kt[l] * 32 * ncol;
                 const float* p = a.dw_part + a.dwp_off[l] + (size_t)k * ncol + j;
-                float s = 0.0f;
-                for (int q = 0; q < a.nparts[l]; ++q) s += p[(size_t)q * slab];
-                v = a.scale ? s * sc : s;
+                v = sum_parts(p, slab, a.nparts[l]);
+                if (a.scale) v *= sc;
             }
             a.d_ws[e] = a.accumulate ? a.d_ws[e] + v : v;
         } else {
@@ -789,9 +805,8 @@ __global__ void grad_reduce_kernel(ReduceArgs a) {
             if (j < a.n[l]) {
                 const int ncol = a.nt[l] * 32;
                 const float* p = a.db_part + a.dbp_off[l] + j;
-                float s = 0.0f;
-                for (int q = 0; q < a.splits[l]; ++q) s += p[(size_t)q * ncol];
-                v = a.scale ? s * sc : s;
+                v = sum_parts(p, (size_t)ncol, a.splits[l]);
+                if (a.scale) v *= sc;
             }
             a.d_bs[eb] = a.accumulate ? a.d_bs[eb] + v : v;
         }

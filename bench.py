@@ -25,6 +25,10 @@ sys.path.insert(0, os.path.join(HERE, "loma-nerf_amd"))
 
 METRIC = "ray-samples/sec fwd+bwd, 4096 rays×64 samples, 1/2/4/8 MI355X"
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA = f32 vector peak (dense)
+# bf16 MFMA dense: 256 CU x 4 SIMD x 1024 FLOP/clk (v_mfma_f32_32x32x16_bf16: 32768 FLOP / 32 clk)
+# x 2.4 GHz = 2516.6 TF; the bf16x6 split spends 6 bf16 MFMA products per fp32 multiply-add
+PEAK_BF16_TFLOPS = 2516.6
+PEAK_X6_TFLOPS = PEAK_BF16_TFLOPS / 6
 PEAK_HBM_GBS = 8000.0
 
 
@@ -39,6 +43,8 @@ def parse():
     ap.add_argument("--cpu-rays", type=int, default=128, help="rays in the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--generic", action="store_true", help="time the loma-order kernels instead")
+    ap.add_argument("--mfma-f32", action="store_true",
+                    help="fused path with exact f32 MFMA products instead of the bf16x6 split")
     return ap.parse_args()
 
 
@@ -121,6 +127,8 @@ def main():
     gbuf = grads[0]
     acc = torch.empty(N, 3, device=dev)
     flags = lnerf.GENERIC if args.generic else lnerf.FAST
+    if args.mfma_f32:
+        flags |= lnerf.MFMA_F32
 
     def step(timing=False):
         f = flags | (lnerf.TIMING if timing else 0)
@@ -173,6 +181,8 @@ def main():
             "metric": METRIC, "value": value, "unit": "ray-samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "mfma": ("generic (no MFMA)" if args.generic else "f32" if args.mfma_f32 else
+                     "bf16x6 (fp32 operands split hi+mid+lo, fp32 accumulate)"),
             "data": "synthetic (look-at camera rays, uniform targets, random-init MLP seed 215)",
             "config": {"workload": f"{args.config}: {N} rays x {S} samples per GPU, PE F={b['F']}, "
                                    f"MLP {shapes[0][0]}->{b['H']}x{b['L'] - 1}->4, fp32",
@@ -182,12 +192,16 @@ def main():
         }
         if kt:
             fus_ms = kt["fused"]
+            peak = PEAK_FP32_TFLOPS if args.mfma_f32 else PEAK_X6_TFLOPS
             out["roofline"] = {"bound": "mfma", "kernel": "fused_fwd_bwd_kernel",
                                "achieved": fused_flops / (fus_ms / 1e3) / 1e12,
-                               "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                               "frac": fused_flops / (fus_ms / 1e3) / 1e12 / PEAK_FP32_TFLOPS,
+                               "peak": peak, "unit": "TFLOP/s",
+                               "frac": fused_flops / (fus_ms / 1e3) / 1e12 / peak,
                                "traffic": None,
-                               "flops_per_launch": fused_flops, "avg_ms": fus_ms}
+                               "flops_per_launch": fused_flops, "avg_ms": fus_ms,
+                               "peak_basis": ("f32 MFMA dense 157.3 TF" if args.mfma_f32 else
+                                              "bf16 MFMA dense 2516.6 TF / 6 (bf16x6: six bf16 "
+                                              "products per fp32-accurate multiply-add)")}
             tr = pmc_traffic("fused_fwd_bwd_kernel", args.config) if args.rays is None else None
             if tr:
                 out["roofline"]["traffic"] = tr["bytes"]
@@ -196,6 +210,7 @@ def main():
                 out["roofline"]["traffic_gbs"] = tr["bytes"] / (fus_ms / 1e3) / 1e9
             out["kernels_ms"] = kt
             out["dw_kernel_tflops"] = dw_flops / (kt["dw"] / 1e3) / 1e12
+            out["dw_kernel_frac"] = out["dw_kernel_tflops"] / peak
         if world == 1 and not args.no_cpu_baseline:
             c1, cn = cpu_baseline(args, args.config)
             out["cpu_baseline"] = c1

@@ -123,7 +123,10 @@ enum {
     LNERF_WANT_DX = 4,        /* also produce d_x (d_layer_input), ENCODED mode only          */
     LNERF_GENERIC = 8,        /* force the stage-by-stage loma-order kernels (no MFMA fusion) */
     LNERF_FAST = 16,          /* require the fused MFMA path (error if the shape is unsupported) */
-    LNERF_TIMING = 32         /* record per-kernel HIP events (read with lnerf_ctx_timings)   */
+    LNERF_TIMING = 32,        /* record per-kernel HIP events (read with lnerf_ctx_timings)   */
+    LNERF_MFMA_F32 = 64       /* fused path: exact f32 MFMA products instead of the default
+                                 bf16x6 split (x = hi+mid+lo in bf16, six bf16 MFMAs per
+                                 product, fp32-accurate: dropped terms <= 2^-24 |w x|)         */
 };
 
 /* Optional outputs (device pointers; any may be NULL). */

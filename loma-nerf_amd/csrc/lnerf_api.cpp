@@ -765,7 +765,7 @@ extern "C" int lnerf_train_step(lnerf_ctx* ctx, const lnerf_mlp* mlp, const floa
         if (use_fused(*mlp, *batch, flags)) {
             const size_t bytes = fused_workspace_bytes(*mlp, batch->rays, batch->samples);
             FusedPlan p{};
-            fused_plan(p, *mlp, *batch, ctx->fused_ws.get(bytes));
+            fused_plan(p, *mlp, *batch, ctx->fused_ws.get(bytes), flags);
             const bool timed = (flags & LNERF_TIMING) != 0;
             fused_train_step(p, ws, bs, *batch, seed, flags, o, s, timed ? ctx->ev : nullptr);
             ctx->timed = timed;
@@ -789,7 +789,7 @@ extern "C" int lnerf_render(lnerf_ctx* ctx, const lnerf_mlp* mlp, const float* w
         if (use_fused(*mlp, *batch, 0)) {
             const size_t bytes = fused_workspace_bytes(*mlp, batch->rays, batch->samples);
             FusedPlan p{};
-            fused_plan(p, *mlp, *batch, ctx->fused_ws.get(bytes));
+            fused_plan(p, *mlp, *batch, ctx->fused_ws.get(bytes), 0);
             fused_render(p, ws, bs, *batch, o, s);
         } else {
             generic_step(ctx, *mlp, ws, bs, *batch, 1.0f, 0, o, false, s);

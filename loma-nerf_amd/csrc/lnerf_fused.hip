@@ -32,7 +32,6 @@ constexpr int kWaves = 4;
 constexpr int kTileSamples = 128;          // samples per fused workgroup
 constexpr int kNT = 8;                     // max 32-wide feature tiles (256 features)
 constexpr int kChunkMax = 16 * 2 * 256;    // floats per staged weight chunk (r x nt4 x 64 lanes x 4)
-constexpr int kMaxMaskLayers = kMaxLayers - 1;
 constexpr int kCompFloats = 24;            // per-sample compositing scratch floats in LDS
 
 // Feature held by accumulator register r of tile t in lane half h (32x32 C/D layout:
@@ -46,8 +45,9 @@ struct FusedArgs {
     int L;
     int kt[kMaxLayers], nt[kMaxLayers];
     int k0;
-    const float* wf;
+    const float* wf;               // f32 MFMA path: fragment-packed weights
     const float* wb;
+    const unsigned short* w6;      // bf16x6 path: split-plane packed weights (u16 offsets)
     const float* bp;
     size_t wf_off[kMaxLayers], wb_off[kMaxLayers], bp_off[kMaxLayers];
     float* act;
@@ -69,38 +69,61 @@ struct FusedArgs {
 };
 
 // ---- LDS carve (one __shared__ array; see cdna_hip_programming.md §5 item 4(a)) --------------
-constexpr int kLdsW = 2 * kChunkMax;                                    // floats
-constexpr int kLdsMaskU64 = kWaves * kMaxMaskLayers * kNT * 16;         // 64-bit words
+// Weight ring: 2 slots of one contraction tile of one layer (f32: 16 regs x 8 tiles x 64 lanes x
+// 4 B = 32 KiB; bf16x6: 2 k-steps x 8 tiles x 3 planes x 64 lanes x 16 B = 48 KiB).
+// ReLU masks: one u64 ballot per (layer, tile, register) per wave, (L-1)*HT tile-layers.
+constexpr int kRingSlotBytes(bool x6) { return x6 ? 2 * kNT * 3 * 1024 : kChunkMax * 4; }
+constexpr int kMaskTiles(bool x6) { return x6 ? 64 : 120; }
 constexpr int kLdsComp = kTileSamples * kCompFloats;                    // floats
 constexpr int kLdsRay = kTileSamples;                                   // per-ray loss partials
 constexpr int kLdsTr = kWaves * 32 * 32;                                // per-wave transpose tile
 constexpr int kLdsBias = 2 * kNT * 32;                                  // 2 x one layer's biases
-constexpr size_t kLdsBytes = (size_t)kLdsW * 4 + (size_t)kLdsMaskU64 * 8 + (size_t)kLdsComp * 4 +
-                             (size_t)kLdsRay * 4 + (size_t)kLdsTr * 4 + (size_t)kLdsBias * 4;
-static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
+constexpr size_t kLdsBytes(bool x6) {
+    return (size_t)2 * kRingSlotBytes(x6) + (size_t)kWaves * kMaskTiles(x6) * 16 * 8 +
+           (size_t)kLdsComp * 4 + (size_t)kLdsRay * 4 + (size_t)kLdsTr * 4 + (size_t)kLdsBias * 4;
+}
+static_assert(kLdsBytes(false) <= 160 * 1024, "LDS budget (f32)");
+static_assert(kLdsBytes(true) <= 160 * 1024, "LDS budget (bf16x6)");
 
 __device__ __forceinline__ int wave_id() {
     return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
 }
 
-// Stage `cf` floats of packed weights into LDS with LDS-DMA (global_load_lds_dwordx4): lane-linear
-// destination, 1 KiB per wave instruction.
-__device__ __forceinline__ void stage_chunk(const float* __restrict__ src, float* dst, int cf) {
+// Stage BYTES (a multiple of 16) of packed weights into LDS with LDS-DMA
+// (global_load_lds_dwordx4): lane-linear destination, 1 KiB per wave instruction.
+// Compile-time size: whole 4-KiB rounds unguarded, one guarded tail round.
+template <int BYTES>
+__device__ __forceinline__ void stage_bytes_t(const void* __restrict__ src, void* dst) {
     const int tid = threadIdx.x, wave = wave_id();
-    for (int base = 0; base < cf; base += kWgThreads * 4) {
-        const float* g = src + base + tid * 4;
-        float* l = dst + base + wave * 256;
+    constexpr int kRound = kWgThreads * 16, kFull = BYTES / kRound, kTail = BYTES % kRound;
+#pragma unroll
+    for (int i = 0; i < kFull; ++i) {
+        const char* g = (const char*)src + i * kRound + tid * 16;
+        char* l = (char*)dst + i * kRound + wave * 1024;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                         (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+    }
+    if (kTail && tid * 16 < kTail) {
+        const char* g = (const char*)src + kFull * kRound + tid * 16;
+        char* l = (char*)dst + kFull * kRound + wave * 1024;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                          (__attribute__((address_space(3))) void*)l, 16, 0, 0);
     }
 }
 
-// Wait for this wave's LDS-DMA (and other vector-memory ops), then barrier: after it every wave's
-// staged bytes are in LDS (explicit, not left to __syncthreads' lowering).
-__device__ __forceinline__ void dma_barrier() {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+// Wait for this wave's LDS-DMA, then s_barrier: afterwards every wave's staged bytes are in LDS.
+// vmcnt(0), not vmcnt(N): on CDNA loads and stores share vmcnt and do not retire in order with
+// respect to each other, so a partial count cannot single out the DMA behind later stores.
+// (__syncthreads would also add lgkmcnt(0); the LDS consumers wait for their own reads.)
+template <int N>
+__device__ __forceinline__ void dma_barrier_n() {
+    static_assert(N == 0, "see above");
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), expcnt(7), lgkmcnt(15)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
 }
+__device__ __forceinline__ void dma_barrier() { dma_barrier_n<0>(); }
 
 // Store one 32x32 accumulator tile (lane = sample, registers = features in C/D order) as a
 // row-major [feature][32 samples] block: transpose through the wave's LDS tile, then 4
@@ -113,7 +136,8 @@ __device__ __forceinline__ void store_tile(const fx16& v, float* __restrict__ ds
     for (int q = 0; q < 4; ++q) {
         const int row = (lane >> 3) + 8 * q, c4 = (lane & 7) * 4;
         const fx4 x = *(const fx4*)(tr + row * 32 + c4);
-        *(fx4*)(dst + row * 32 + c4) = x;
+        // streaming store (nt): the slabs are read once, by the dW kernel; keep L2 for weights
+        __builtin_nontemporal_store(x, (fx4*)(dst + row * 32 + c4));
     }
 }
 
@@ -136,7 +160,7 @@ __device__ __forceinline__ void mma_stream_t(const float* __restrict__ src, int 
     const int lane = threadIdx.x & 63;
     constexpr int NT4 = (NTO + 3) / 4;
     constexpr int CF = 16 * NT4 * 256;
-    stage_chunk(src, ldsw, CF);
+    stage_bytes_t<CF * 4>(src, ldsw);
     if (bias_src && wave_id() == 0)
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bias_src + lane * 4),
                                          (__attribute__((address_space(3))) void*)bias_lds, 16, 0, 0);
@@ -144,10 +168,10 @@ __device__ __forceinline__ void mma_stream_t(const float* __restrict__ src, int 
 #pragma unroll
     for (int c = 0; c < (NCH > 0 ? NCH : kNT); ++c) {
         if (NCH > 0 || c < nchunks) {
-            if (tstore && c >= 1) store_tile(in[c - 1], tstore + (c - 1) * 1024, tr);
             const float* cur = ldsw + (c & 1) * kChunkMax + lane * 4;
             if (c + 1 < nchunks)
-                stage_chunk(src + (size_t)(c + 1) * CF, ldsw + ((c + 1) & 1) * kChunkMax, CF);
+                stage_bytes_t<CF * 4>(src + (size_t)(c + 1) * CF, ldsw + ((c + 1) & 1) * kChunkMax);
+            if (tstore && c >= 1) store_tile(in[c - 1], tstore + (c - 1) * 1024, tr);
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 fx4 w[NT4];
@@ -164,13 +188,131 @@ __device__ __forceinline__ void mma_stream_t(const float* __restrict__ src, int 
 }
 
 // Output-tile counts are rounded up to 1/2/4/8 (the padded tiles of the packed weights are zero).
-__device__ __forceinline__ void mma_stream(const float* __restrict__ src, int nchunks, int nto,
-                                           const fx16 (&in)[kNT], fx16 (&out)[kNT], float* ldsw,
-                                           float* tstore, float* tr) {
-    if (nto <= 1) mma_stream_t<1>(src, nchunks, in, out, ldsw, tstore, tr, nullptr, nullptr);
-    else if (nto <= 2) mma_stream_t<2>(src, nchunks, in, out, ldsw, tstore, tr, nullptr, nullptr);
-    else if (nto <= 4) mma_stream_t<4>(src, nchunks, in, out, ldsw, tstore, tr, nullptr, nullptr);
-    else mma_stream_t<8>(src, nchunks, in, out, ldsw, tstore, tr, nullptr, nullptr);
+template <bool X6>
+__device__ __forceinline__ void layer_mma_n(const FusedArgs& a, bool fwd, int l, int nchunks, int nto,
+                                            const fx16 (&in)[kNT], fx16 (&out)[kNT],
+                                            unsigned char* ring, float* tstore, float* tr);
+
+// ---- bf16x6: fp32-accurate products on the bf16 MFMA ---------------------------------------
+// x = hi + mid + lo, each a bf16 (8 significant bits; round-to-nearest, the remainders are exact in
+// f32), so the three planes carry x's 24 bits. A product keeps the six terms down to 2^-16
+// relative (hh, hm, mh, hl, lh, mm): the dropped terms are <= 2^-24 |w x|, fp32 rounding size.
+// v_mfma_f32_32x32x16_bf16 does 16x the FLOP/cycle of v_mfma_f32_32x32x2_f32, so six of them
+// are 2.67x the f32 rate (MI355X_MICROARCH.md § Matrix cores).
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split3(const fx16& v, int s, bf8& hi, bf8& mid, bf8& lo) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float x = v[8 * s + j];
+        const __bf16 h = (__bf16)x;
+        const float r = x - (float)h;
+        const __bf16 m = (__bf16)r;
+        hi[j] = h;
+        mid[j] = m;
+        lo[j] = (__bf16)(r - (float)m);
+    }
+}
+
+__device__ __forceinline__ fx16 mfma_x6(const bf8& wh, const bf8& wm, const bf8& wl, const bf8& bh,
+                                        const bf8& bm, const bf8& bl, fx16 acc) {
+    // small terms first (in the order the planes arrive from LDS: hi, mid, lo)
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, bl, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wm, bm, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, bh, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wm, bh, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, bm, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, bh, acc, 0, 0, 0);
+    return acc;
+}
+
+// bf16x6 form of mma_stream_t. Packed chunk c (= contraction tile c) of a layer holds, for k-step
+// s (16 of the tile's 32 features), output tile o and plane p, one 16-B A fragment per lane:
+// [s][o][p][lane][8 x bf16], the 8 k's of lane half h being the features that accumulator
+// registers 8s..8s+7 of the input tile hold (cdna_hip_programming.md "accumulator tile as the
+// next MFMA's operand"). The B operand is the input tile itself, split into planes on the fly.
+template <int NTO>
+__device__ __forceinline__ void mma_stream_x6(const unsigned short* __restrict__ src, int nchunks,
+                                              const fx16 (&in)[kNT], fx16 (&out)[kNT],
+                                              unsigned char* ring, float* tstore, float* tr,
+                                              const float* bias_src, float* bias_lds) {
+    const int lane = threadIdx.x & 63;
+    constexpr int CB = 2 * NTO * 3 * 1024;        // bytes per chunk
+    constexpr int SLOT = kRingSlotBytes(true);
+    stage_bytes_t<CB>(src, ring);
+    if (bias_src && wave_id() == 0)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bias_src + lane * 4),
+                                         (__attribute__((address_space(3))) void*)bias_lds, 16, 0, 0);
+    dma_barrier();
+#pragma unroll
+    for (int c = 0; c < kNT; ++c) {
+        if (c < nchunks) {
+            const unsigned char* cur = ring + (c & 1) * SLOT + lane * 16;
+            if (c + 1 < nchunks)
+                stage_bytes_t<CB>((const char*)src + (size_t)(c + 1) * CB, ring + ((c + 1) & 1) * SLOT);
+            if (tstore && c >= 1) store_tile(in[c - 1], tstore + (c - 1) * 1024, tr);
+            // retire any scalar (kernarg) loads still in flight: while one is pending the
+            // waitcnt pass can only emit lgkmcnt(0) for the LDS fragment reads below
+            __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0), vmcnt/expcnt untouched
+            __builtin_amdgcn_sched_barrier(0);
+            // software-pipelined two steps deep: the three planes of step i+2 are read while
+            // step i's six MFMAs run, so a step's fragments have had a whole step to land
+            constexpr int NS = 2 * NTO;
+            bf8 bp[2][3];
+            split3(in[c], 0, bp[0][0], bp[0][1], bp[0][2]);
+            bf8 w[NS][3];
+#pragma unroll
+            for (int i = 0; i < 2 && i < NS; ++i)
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) w[i][pl] = *(const bf8*)(cur + (i * 3 + pl) * 1024);
+#pragma unroll
+            for (int i = 0; i < NS; ++i) {
+                const int ks = i / NTO, o = i % NTO;
+                if (i + 2 < NS) {
+#pragma unroll
+                    for (int pl = 0; pl < 3; ++pl)
+                        w[i + 2][pl] = *(const bf8*)(cur + ((i + 2) * 3 + pl) * 1024);
+                }
+                if (i == 0) split3(in[c], 1, bp[1][0], bp[1][1], bp[1][2]);
+                out[o] = mfma_x6(w[i][0], w[i][1], w[i][2], bp[ks][0], bp[ks][1], bp[ks][2], out[o]);
+            }
+            // pin that order for the scheduler: [reads of steps 0, 1], then per step i the
+            // reads of step i+2 followed by the six MFMAs of step i
+            __builtin_amdgcn_sched_group_barrier(0x100, NS >= 2 ? 6 : 3, 0);
+#pragma unroll
+            for (int i = 0; i < NS; ++i) {
+                if (i + 2 < NS) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+            }
+            dma_barrier();
+            if (tstore && c == nchunks - 1) store_tile(in[c], tstore + c * 1024, tr);
+        }
+    }
+}
+
+// One layer's MMA in either precision (X6: bf16x6 split planes; else exact f32 MFMA).
+template <int NTO, bool X6>
+__device__ __forceinline__ void layer_mma(const FusedArgs& a, bool fwd, int l, int nchunks,
+                                          const fx16 (&in)[kNT], fx16 (&out)[kNT],
+                                          unsigned char* ring, float* tstore, float* tr,
+                                          const float* bias_src, float* bias_lds) {
+    if (X6) {
+        const unsigned short* src = a.w6 + (fwd ? a.wf_off[l] : a.wb_off[l]);
+        mma_stream_x6<NTO>(src, nchunks, in, out, ring, tstore, tr, bias_src, bias_lds);
+    } else {
+        const float* src = fwd ? a.wf + a.wf_off[l] : a.wb + a.wb_off[l];
+        mma_stream_t<NTO>(src, nchunks, in, out, (float*)ring, tstore, tr, bias_src, bias_lds);
+    }
+}
+
+template <bool X6>
+__device__ __forceinline__ void layer_mma_n(const FusedArgs& a, bool fwd, int l, int nchunks, int nto,
+                                            const fx16 (&in)[kNT], fx16 (&out)[kNT],
+                                            unsigned char* ring, float* tstore, float* tr) {
+    if (nto <= 1) layer_mma<1, X6>(a, fwd, l, nchunks, in, out, ring, tstore, tr, nullptr, nullptr);
+    else if (nto <= 2) layer_mma<2, X6>(a, fwd, l, nchunks, in, out, ring, tstore, tr, nullptr, nullptr);
+    else if (nto <= 4) layer_mma<4, X6>(a, fwd, l, nchunks, in, out, ring, tstore, tr, nullptr, nullptr);
+    else layer_mma<8, X6>(a, fwd, l, nchunks, in, out, ring, tstore, tr, nullptr, nullptr);
 }
 
 __device__ __forceinline__ float input_feature(const FusedArgs& a, int gs, bool valid, int f) {
@@ -185,128 +327,175 @@ __device__ __forceinline__ float input_feature(const FusedArgs& a, int gs, bool 
     return (fb & 1) ? (float)cos(arg) : (float)sin(arg);
 }
 
-// One ray: rendering (nerf.py:176-302) and its reverse with loma's statement order (see
-// lnerf_generic.hip, lg_composite_fwd/bwd), on LDS scratch. z = head pre-activations [S][4].
-struct RayScratch {
-    float* z;      // [S][4] head pre-activation
-    float* rgba;   // [S][4]
-    float* al;     // [S]
-    float* cC;     // [S]
-    float* cP;     // [S]
-    float* cT;     // [S]
-    float* w;      // [S]
-    float* dw;     // [S]
-    float* dal;    // [S]
-    float* dcp;    // [S]
-    float* drgba;  // [S][4]
-    float* gz;     // [S][4] output: dL/dz head
-};
-
-__device__ __forceinline__ float composite_ray(const FusedArgs& a, int ray, const RayScratch& s,
-                                             bool grad) {
-    const int S = a.S;
-    const float* dists = a.dists + (size_t)ray * S;
-    // head activation (nerf.py:153-167): channel 3 ReLU, 0..2 sigmoid
-    for (int j = 0; j < S; ++j)
-        for (int k = 0; k < 4; ++k) {
-            const float v = s.z[j * 4 + k];
-            s.rgba[j * 4 + k] = (k == 3) ? ((v > 0.0f) ? v : 0.0f) : 1.0f / (1.0f + expf(0.0f - v));
+// ---- rendering (nerf.py:176-302), loss and its reverse for one 128-sample tile ----------------
+// One thread per sample (threads 0..127; a ray = S consecutive samples = one scan segment), the
+// along-ray dependencies as segmented Hillis-Steele scans in LDS (log2 S rounds):
+//   forward  P_j = prod_{i<=j} c_i (inclusive, T_0 = 1, T_j = P_j: nerf.py:226-272),
+//            C = sum_j w_j rgb_j (segmented sum, read at the ray's last sample);
+//   reverse  G_j = a_j + c_{j+1} G_{j+1} (the reverse of the inclusive cumprod,
+//            a_j = alpha_j dL/dw_j for j >= 1), dc_j = P_{j-1} G_j, dc_0 = G_0.
+// Every per-sample expression is loma's (composite rules of lnerf_generic.hip); only the
+// association of the along-ray products and sums differs from loma's sequential loops, at fp32
+// rounding level (the parity tolerance covers it; the generic path keeps the exact order).
+// LDS: comp[0..512) z [128][4] (in), [512..1024) gz [128][4] (out), two [4][128] ping-pong scan
+// buffers at 1024 / 1536, P at 2048, per-ray dacc [128][4] at 2176 (kCompFloats = 24 per sample).
+__device__ __forceinline__ void seg_scan_fwd(float* buf0, float* buf1, int ls, int j, int S, int nv,
+                                             float (&v)[4], bool prod_first) {
+    // inclusive segmented scan of nv values (v[0] by product if prod_first, the rest by sum)
+    float* cur = buf0;
+    float* nxt = buf1;
+    for (int d = 1; d < S; d <<= 1) {
+        if (ls < kTileSamples)
+            for (int q = 0; q < nv; ++q) cur[q * kTileSamples + ls] = v[q];
+        __syncthreads();
+        if (ls < kTileSamples && j >= d) {
+            for (int q = 0; q < nv; ++q) {
+                const float o = cur[q * kTileSamples + ls - d];
+                v[q] = (q == 0 && prod_first) ? o * v[q] : o + v[q];
+            }
         }
-    for (int j = 0; j < S; ++j) s.al[j] = 1.0f - expf((0.0f - s.rgba[j * 4 + 3]) * dists[j]);
-    for (int j = 0; j < S; ++j) s.cC[j] = (1.0f - s.al[j]) + (float)(1e-10);
-    float p = 0.0f;
-    for (int j = 0; j < S; ++j) {
-        p = (j == 0) ? s.cC[0] : p * s.cC[j];
-        s.cP[j] = p;
-        s.cT[j] = (j == 0) ? 1.0f : p;
+        float* t = cur;
+        cur = nxt;
+        nxt = t;
     }
-    for (int j = 0; j < S; ++j) s.w[j] = s.al[j] * s.cT[j];
-    float acc0 = 0.0f, acc1 = 0.0f, acc2 = 0.0f;
-    for (int j = 0; j < S; ++j) {
-        acc0 = acc0 + s.w[j] * s.rgba[j * 4 + 0];
-        acc1 = acc1 + s.w[j] * s.rgba[j * 4 + 1];
-        acc2 = acc2 + s.w[j] * s.rgba[j * 4 + 2];
+    __syncthreads();   // the next scan may write the buffer this one read last
+}
+
+__device__ __forceinline__ float composite_tile(const FusedArgs& a, int wg, float* comp, float* rayloss,
+                                                bool grad) {
+    const int tid = threadIdx.x, S = a.S;
+    float* c_z = comp;
+    float* c_gz = comp + 512;
+    float* sb0 = comp + 1024;
+    float* sb1 = comp + 1536;
+    float* c_P = comp + 2048;
+    float* c_ray = comp + 2176;               // [128 rays][4]: dacc0..2 of each ray
+    const int ntile = a.rpw * S;              // samples of whole rays in this tile
+    const int ls = tid < kTileSamples ? tid : kTileSamples;   // threads >= 128 only sync
+    const int rl = ls / S, j = ls - rl * S;   // ray within the tile, sample within the ray
+    const int ray = wg * a.rpw + rl;
+    const bool valid = ls < ntile && ray < a.rays;
+    const size_t gs = (size_t)ray * S + j;
+    float z[4] = {0, 0, 0, 0}, rgb[3] = {0, 0, 0}, sigma = 0, delta = 0, al = 0, cc = 1;
+    if (valid) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) z[k] = c_z[ls * 4 + k];
+        // head activation (nerf.py:153-167): channel 3 ReLU, 0..2 sigmoid
+#pragma unroll
+        for (int k = 0; k < 3; ++k) rgb[k] = 1.0f / (1.0f + expf(0.0f - z[k]));
+        sigma = (z[3] > 0.0f) ? z[3] : 0.0f;
+        delta = a.dists[gs];
+        al = 1.0f - expf((0.0f - sigma) * delta);
+        cc = (1.0f - al) + (float)(1e-10);
     }
-    const float* t = a.target + (size_t)ray * 3;
+    // P_j (inclusive product), T_j, w_j
+    float v[4] = {cc, 0, 0, 0};
+    seg_scan_fwd(sb0, sb1, ls, j, S, 1, v, true);
+    const float P = v[0];
+    const float T = (j == 0) ? 1.0f : P;
+    const float w = al * T;
+    if (ls < kTileSamples) c_P[ls] = P;
+    // colour: segmented sum of w * rgb (read at the ray's last sample)
+    float cv[4] = {w * rgb[0], w * rgb[1], w * rgb[2], 0};
+    seg_scan_fwd(sb0, sb1, ls, j, S, 3, cv, false);
     float loss = 0.0f;
-    loss = loss + (acc0 - t[0]) * (acc0 - t[0]);
-    loss = loss + (acc1 - t[1]) * (acc1 - t[1]);
-    loss = loss + (acc2 - t[2]) * (acc2 - t[2]);
-    if (a.acc_color) {
-        a.acc_color[(size_t)ray * 3 + 0] = acc0;
-        a.acc_color[(size_t)ray * 3 + 1] = acc1;
-        a.acc_color[(size_t)ray * 3 + 2] = acc2;
-    }
-    if (!grad) return loss;
-
-    // ---- reverse (lg_composite_bwd_kernel with zero incoming adjoints) ----
-    const float seed = a.seed;
-    float dacc[3] = {0.0f, 0.0f, 0.0f};
-    const float accv[3] = {acc0, acc1, acc2};
-    for (int c = 2; c >= 0; --c) {
-        const float a1 = (accv[c] - t[c]) * seed;
-        const float a2 = 0.0f - ((accv[c] - t[c]) * seed);
-        dacc[c] += a1;
-        dacc[c] += a1;
-        if (a.d_target) a.d_target[(size_t)ray * 3 + c] = (0.0f + a2) + a2;
-    }
-    for (int j = 0; j < S; ++j) {
-        s.dw[j] = 0.0f;
-        s.dal[j] = 0.0f;
-        s.dcp[j] = 0.0f;
-        for (int k = 0; k < 4; ++k) s.drgba[j * 4 + k] = 0.0f;
-    }
-    for (int j = S - 1; j >= 0; --j)
-        for (int c = 2; c >= 0; --c) {
-            s.dw[j] += s.rgba[j * 4 + c] * dacc[c];
-            s.drgba[j * 4 + c] += s.w[j] * dacc[c];
+    const bool last = valid && j == S - 1;
+    if (last) {
+        const float* t = a.target + (size_t)ray * 3;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            loss = loss + (cv[k] - t[k]) * (cv[k] - t[k]);
+            if (a.acc_color) a.acc_color[(size_t)ray * 3 + k] = cv[k];
         }
-    for (int j = S - 1; j >= 0; --j) {
-        const float adj = s.dw[j];
-        s.dal[j] += s.cT[j] * adj;
-        s.dcp[j] += s.al[j] * adj;
+        if (grad) {
+            // reverse of the loss (lg_composite_bwd_kernel): dacc = 2 seed (C - t)
+            for (int k = 2; k >= 0; --k) {
+                const float a1 = (cv[k] - t[k]) * a.seed;
+                const float a2 = 0.0f - ((cv[k] - t[k]) * a.seed);
+                c_ray[rl * 4 + k] = 0.0f + a1 + a1;
+                if (a.d_target) a.d_target[(size_t)ray * 3 + k] = (0.0f + a2) + a2;
+            }
+        }
     }
-    s.dcp[0] = 0.0f;                                   // T_0 = 1
-    for (int j = S - 1; j >= 1; --j) {                 // inclusive cumprod reverse
-        const float adj = s.dcp[j];
-        const float a_left = s.cC[j] * adj;
-        const float a_right = s.cP[j - 1] * adj;
-        s.dcp[j] = 0.0f;
-        s.dcp[j - 1] += a_left;
-        s.dcp[j] += a_right;
+    if (tid < a.rpw) rayloss[tid] = 0.0f;
+    __syncthreads();
+    if (last) rayloss[rl] = loss;
+    if (!grad) return 0.0f;
+
+    // ---- reverse, per sample ----
+    float dacc[3] = {0, 0, 0}, dw = 0.0f, drgb[4] = {0, 0, 0, 0};
+    if (valid) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) dacc[k] = c_ray[rl * 4 + k];
+        for (int k = 2; k >= 0; --k) {
+            dw += rgb[k] * dacc[k];
+            drgb[k] += w * dacc[k];
+        }
     }
-    for (int j = S - 1; j >= 0; --j) s.dal[j] += 0.0f - s.dcp[j];   // cumprod init reverse
-    for (int j = S - 1; j >= 0; --j) {                               // alpha reverse
-        const float sigma = s.rgba[j * 4 + 3], delta = dists[j];
-        const float adj2 = (0.0f - s.dal[j]) * expf((0.0f - sigma) * delta);
-        s.drgba[j * 4 + 3] += 0.0f - (delta * adj2);
-        if (a.d_dists) a.d_dists[(size_t)ray * S + j] = 0.0f + (0.0f - sigma) * adj2;
+    float dal = T * dw;
+    // G_j = a_j + c_{j+1} G_{j+1}: segmented suffix scan of (a, b) pairs
+    float ga = (j >= 1) ? al * dw : 0.0f;
+    float gb = 0.0f;
+    if (ls < kTileSamples) sb0[ls] = cc;
+    __syncthreads();
+    if (valid && j + 1 < S) gb = sb0[ls + 1];
+    __syncthreads();
+    {
+        float* cur = sb0;
+        float* nxt = sb1;
+        for (int d = 1; d < S; d <<= 1) {
+            if (ls < kTileSamples) {
+                cur[ls] = ga;
+                cur[kTileSamples + ls] = gb;
+            }
+            __syncthreads();
+            if (ls < kTileSamples && j + d < S) {
+                const float oa = cur[ls + d], ob = cur[kTileSamples + ls + d];
+                ga = ga + gb * oa;
+                gb = gb * ob;
+            }
+            float* t = cur;
+            cur = nxt;
+            nxt = t;
+        }
     }
-    // head activation reverse (reverse_diff.py Div/exp/Sub rules; ReLU on the post value)
-    for (int j = 0; j < S; ++j)
+    if (valid) {
+        const float dc = (j >= 1) ? c_P[ls - 1] * ga : ga;
+        dal += 0.0f - dc;                                       // cC = (1 - al) + 1e-10
+        const float adj2 = (0.0f - dal) * expf((0.0f - sigma) * delta);   // alpha reverse
+        drgb[3] += 0.0f - (delta * adj2);
+        if (a.d_dists) a.d_dists[gs] = 0.0f + (0.0f - sigma) * adj2;
+        // head activation reverse (reverse_diff.py Div/exp/Sub rules; ReLU on the post value)
+#pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const float dz = s.drgba[j * 4 + k];
+            const float dz = drgb[k];
             float g;
             if (k == 3) {
-                g = (s.rgba[j * 4 + 3] > 0.0f) ? dz : 0.0f;
+                g = (sigma > 0.0f) ? dz : 0.0f;
             } else {
-                const float x = s.z[j * 4 + k];
+                const float x = z[k];
                 const float u = 1.0f + expf(0.0f - x);
                 const float adj_div = ((0.0f - dz) * 1.0f) / (u * u);
                 g = 0.0f + (0.0f - adj_div * expf(0.0f - x));
             }
-            s.gz[j * 4 + k] = g;
+            c_gz[ls * 4 + k] = g;
         }
-    return loss;
+    } else if (ls < kTileSamples) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) c_gz[ls * 4 + k] = 0.0f;
+    }
+    return 0.0f;
 }
 
 // HT = output tiles of every hidden layer (widths <= 32*HT); the head has <= 32 outputs.
-template <int HT>
+// X6: bf16x6 split-plane MFMA (fp32-accurate, 2.67x the f32 MFMA rate); else exact f32 MFMA.
+template <int HT, bool X6>
 __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs a) {
-    __shared__ __attribute__((aligned(16))) unsigned char lds_raw[kLdsBytes];
+    __shared__ __attribute__((aligned(16))) unsigned char lds_raw[kLdsBytes(X6)];
+    unsigned char* ring = lds_raw;
     float* ldsw = (float*)lds_raw;
-    unsigned long long* masks = (unsigned long long*)(lds_raw + (size_t)kLdsW * 4);
-    float* comp = (float*)(lds_raw + (size_t)kLdsW * 4 + (size_t)kLdsMaskU64 * 8);
+    unsigned long long* masks = (unsigned long long*)(lds_raw + 2 * (size_t)kRingSlotBytes(X6));
+    float* comp = (float*)((unsigned char*)masks + (size_t)kWaves * kMaskTiles(X6) * 16 * 8);
     float* rayloss = comp + kLdsComp;
     float* trall = rayloss + kLdsRay;
     float* biasl = trall + kLdsTr;
@@ -318,7 +507,7 @@ __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs 
     const int gs = wg * tile_samples + ls;            // global sample row (ray*S + j)
     const bool valid = (ls < tile_samples) && (gs < a.R);
     const size_t blk = (size_t)wg * kWaves + wave;    // 32-sample slab index
-    unsigned long long* wmask = masks + (size_t)wave * kMaxMaskLayers * kNT * 16;
+    unsigned long long* wmask = masks + (size_t)wave * kMaskTiles(X6) * 16;   // [(l*HT + o)][16]
     float* tr = trall + wave * 1024;
     const bool st = a.want_grad != 0;
 
@@ -356,8 +545,8 @@ __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs 
                                   : a.act + a.act_off[l - 1] + blk * (size_t)(a.kt[l] * 1024));
         float* bl = biasl + (l & 1) * (kNT * 32);
         // hidden layers l >= 1 and the head contract over HT tiles (k_l = n_{l-1})
-        if (l < a.L - 1) mma_stream_t<HT>(a.wf + a.wf_off[l], a.kt[l], act, out, ldsw, ts, tr, a.bp + a.bp_off[l], bl);
-        else mma_stream_t<1>(a.wf + a.wf_off[l], a.kt[l], act, out, ldsw, ts, tr, a.bp + a.bp_off[l], bl);
+        if (l < a.L - 1) layer_mma<HT, X6>(a, true, l, a.kt[l], act, out, ring, ts, tr, a.bp + a.bp_off[l], bl);
+        else layer_mma<1, X6>(a, true, l, a.kt[l], act, out, ring, ts, tr, a.bp + a.bp_off[l], bl);
         if (l < a.L - 1) {
 #pragma unroll
             for (int o = 0; o < HT; ++o) {
@@ -372,7 +561,7 @@ __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs 
                 }
                 if (lane == 0) {
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) wmask[((size_t)l * kNT + o) * 16 + r] = m[r];
+                    for (int r = 0; r < 16; ++r) wmask[((size_t)l * HT + o) * 16 + r] = m[r];
                 }
             }
 #pragma unroll
@@ -387,35 +576,9 @@ __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs 
     }
     __syncthreads();
 
-    // ---- rendering + loss + rendering reverse: one thread per ray ----
-    // comp (struct of arrays over the tile's 128 local samples; ray-major like the samples)
-    float* c_z = comp;                          // [128][4]  (written by the head epilogue)
-    float* c_rgba = comp + kTileSamples * 4;    // [128][4]
-    float* c_drgba = comp + kTileSamples * 8;   // [128][4]
-    float* c_gz = comp + kTileSamples * 12;     // [128][4]
-    float* c_vec = comp + kTileSamples * 16;    // 8 x [128]
-    if (tid < a.rpw) {
-        const int ray = wg * a.rpw + tid;
-        float loss = 0.0f;
-        if (ray < a.rays) {
-            const int o = tid * a.S;
-            RayScratch s;
-            s.z = c_z + o * 4;
-            s.rgba = c_rgba + o * 4;
-            s.drgba = c_drgba + o * 4;
-            s.gz = c_gz + o * 4;
-            s.al = c_vec + 0 * kTileSamples + o;
-            s.cC = c_vec + 1 * kTileSamples + o;
-            s.cP = c_vec + 2 * kTileSamples + o;
-            s.cT = c_vec + 3 * kTileSamples + o;
-            s.w = c_vec + 4 * kTileSamples + o;
-            s.dw = c_vec + 5 * kTileSamples + o;
-            s.dal = c_vec + 6 * kTileSamples + o;
-            s.dcp = c_vec + 7 * kTileSamples + o;
-            loss = composite_ray(a, ray, s, a.want_grad != 0);
-        }
-        rayloss[tid] = loss;
-    }
+    // ---- rendering + loss + rendering reverse: one thread per sample, scans along rays ----
+    float* c_gz = comp + 512;
+    composite_tile(a, wg, comp, rayloss, a.want_grad != 0);
     __syncthreads();
     if (tid == 0) {
         float l = 0.0f;
@@ -440,12 +603,12 @@ __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs 
 #pragma unroll
         for (int o = 0; o < kNT; ++o) out[o] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         float* ts = a.grad + a.grad_off[l] + blk * (size_t)(a.nt[l] * 1024);
-        mma_stream_t<HT>(a.wb + a.wb_off[l], a.nt[l], act, out, ldsw, ts, tr, nullptr, nullptr);
+        layer_mma<HT, X6>(a, false, l, a.nt[l], act, out, ring, ts, tr, nullptr, nullptr);
 #pragma unroll
         for (int o = 0; o < HT; ++o) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const unsigned long long m = wmask[((size_t)(l - 1) * kNT + o) * 16 + r];
+                const unsigned long long m = wmask[((size_t)(l - 1) * HT + o) * 16 + r];
                 act[o][r] = ((m >> lane) & 1ull) ? out[o][r] : 0.0f;
             }
         }
@@ -459,7 +622,7 @@ __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs 
         // also writes G_0's slab
 #pragma unroll
         for (int o = 0; o < kNT; ++o) out[o] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        mma_stream(a.wb + a.wb_off[0], a.nt[0], a.kt[0], act, out, ldsw, g0, tr);
+        layer_mma_n<X6>(a, false, 0, a.nt[0], a.kt[0], act, out, ring, g0, tr);
         if (valid) {
 #pragma unroll
             for (int o = 0; o < kNT; ++o)
@@ -554,11 +717,55 @@ __device__ __forceinline__ void dw_block(const float* ca, const float* cg, int k
     }
 }
 
+// bf16x6 form of dw_block: a k-step is 16 samples (lane half h: samples 16ks + 8h + j), the
+// fp32 slab values split into hi/mid/lo planes after the LDS read (each split feeds TJ or TI
+// tiles x 6 MFMAs). Two k-steps per 32-sample slab.
+__device__ __forceinline__ void split3_8(const fx4& x0, const fx4& x1, bf8& hi, bf8& mid, bf8& lo) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float x = j < 4 ? x0[j] : x1[j - 4];
+        const __bf16 hh = (__bf16)x;
+        const float r = x - (float)hh;
+        const __bf16 m = (__bf16)r;
+        hi[j] = hh;
+        mid[j] = m;
+        lo[j] = (__bf16)(r - (float)m);
+    }
+}
+
+template <int TI, int TJ>
+__device__ __forceinline__ void dw_block_x6(const float* ca, const float* cg, int kb, int jb,
+                                            fx16 (&acc)[TI][TJ]) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, rl = lane & 31;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+        bf8 ap[TI][3], gp[TJ][3];
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+            const int row = (kb + i) * 32 + rl;
+            const fx4 x0 = dw_frag(ca, row, 2 * ks, h), x1 = dw_frag(ca, row, 2 * ks + 1, h);
+            // dw_frag(g) reads chunk 2g + h: samples 8g + 4h.. -> here chunks 4ks + h, 4ks + 2 + h
+            split3_8(x0, x1, ap[i][0], ap[i][1], ap[i][2]);
+        }
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+            const int row = (jb + j) * 32 + rl;
+            const fx4 x0 = dw_frag(cg, row, 2 * ks, h), x1 = dw_frag(cg, row, 2 * ks + 1, h);
+            split3_8(x0, x1, gp[j][0], gp[j][1], gp[j][2]);
+        }
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+                acc[i][j] = mfma_x6(ap[i][0], ap[i][1], ap[i][2], gp[j][0], gp[j][1], gp[j][2], acc[i][j]);
+    }
+}
+
 // The whole per-workgroup pass for one layer. PHASED = false: wave w owns a 4x4 block of the
 // layer's output tiles and every sample; PHASED = true (small layers, TI*TJ <= 16 tiles): every
 // wave owns all TI x TJ tiles and one of the 4 sample steps of each slab, writing its own
 // partial (4 partials per split). Each instantiation keeps its accumulators to itself.
-template <int TI, int TJ, bool PHASED>
+template <int TI, int TJ, bool PHASED, bool X6>
 __device__ __forceinline__ void dw_run(const DwArgs a, int l, int sp, float* lds) {
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -605,7 +812,8 @@ __device__ __forceinline__ void dw_run(const DwArgs a, int l, int sp, float* lds
         const float* cg = cur + kDwRows * 32;
         // (unconditional: a branch around the MFMAs makes the compiler shuttle the accumulators
         // between AGPRs and VGPRs every slab)
-        dw_block<TI, TJ>(ca, cg, kb, jb, g0, g1, acc);
+        if (X6) dw_block_x6<TI, TJ>(ca, cg, kb, jb, acc);
+        else dw_block<TI, TJ>(ca, cg, kb, jb, g0, g1, acc);
         if (tid < g_rows) {
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
@@ -643,21 +851,25 @@ __device__ __forceinline__ void dw_run(const DwArgs a, int l, int sp, float* lds
 
 // One launch per group of layers sharing an instantiation (all blocked layers together, each
 // phased shape on its own), so no kernel merges different accumulator sets.
-template <int TI, int TJ, bool PHASED>
+// X6: bf16x6 products (blocked layers only; the small phased layers stay on f32 MFMA).
+template <int TI, int TJ, bool PHASED, bool X6>
 __global__ void __launch_bounds__(kWgThreads, 1) dw_kernel(DwArgs a) {
     __shared__ __attribute__((aligned(16))) float lds[2 * kDwStageFloats];
     int i = 0;
     while (i + 1 < a.nl && (int)blockIdx.x >= a.wg_off[i + 1]) ++i;
-    dw_run<TI, TJ, PHASED>(a, a.lid[i], blockIdx.x - a.wg_off[i], lds);
+    dw_run<TI, TJ, PHASED, X6>(a, a.lid[i], blockIdx.x - a.wg_off[i], lds);
 }
 
-void launch_dw(int mode, int grid, const DwArgs& a, hipStream_t s) {
+void launch_dw(int mode, int grid, const DwArgs& a, bool x6, hipStream_t s) {
     switch (mode) {
 #define LNERF_DW_CASE(I, J, M) \
-    case M: dw_kernel<I, J, true><<<grid, kWgThreads, 0, s>>>(a); break;
+    case M: dw_kernel<I, J, true, false><<<grid, kWgThreads, 0, s>>>(a); break;
         LNERF_DW_PHASED_SHAPES(LNERF_DW_CASE)
 #undef LNERF_DW_CASE
-        default: dw_kernel<4, 4, false><<<grid, kWgThreads, 0, s>>>(a); break;
+        default:
+            if (x6) dw_kernel<4, 4, false, true><<<grid, kWgThreads, 0, s>>>(a);
+            else dw_kernel<4, 4, false, false><<<grid, kWgThreads, 0, s>>>(a);
+            break;
     }
 }
 
@@ -675,14 +887,17 @@ int dw_mode_for(int kt, int nt) {
 struct PackArgs {
     int L;
     int k[kMaxLayers], n[kMaxLayers], kt[kMaxLayers], nt[kMaxLayers];
+    int fo[kMaxLayers], bo[kMaxLayers];   // output tiles the kernel's MMA runs (padded, see Layout)
     int w_k, w_n;
     const float* W;
     const float* B;
     float* wf;
     float* wb;
     float* bp;
+    unsigned short* w6;
     size_t wf_off[kMaxLayers], wb_off[kMaxLayers], bp_off[kMaxLayers];
     size_t wf_n[kMaxLayers], wb_n[kMaxLayers], bp_n[kMaxLayers];
+    size_t w6f_off[kMaxLayers], w6b_off[kMaxLayers], w6f_n[kMaxLayers], w6b_n[kMaxLayers];
 };
 
 __global__ void pack_kernel(PackArgs a, int l) {
@@ -693,7 +908,7 @@ __global__ void pack_kernel(PackArgs a, int l) {
          e += (size_t)gridDim.x * blockDim.x) {
         if (e < nf) {
             // WF[t][r][jt4][lane][e4] = W[f(t,r,h)][32 jt + lane&31]
-            const int nt4 = (a.nt[l] + 3) >> 2;
+            const int nt4 = (a.fo[l] + 3) >> 2;
             size_t x = e;
             const int e4 = x & 3; x >>= 2;
             const int ln = x & 63; x >>= 6;
@@ -705,7 +920,7 @@ __global__ void pack_kernel(PackArgs a, int l) {
         } else if (e < nf + nb) {
             // WB[jt][r][kt4][lane][e4] = W[32 kt + lane&31][f(jt,r,h)]
             const size_t eb = e - nf;
-            const int kt4n = (a.kt[l] + 3) >> 2;
+            const int kt4n = (a.bo[l] + 3) >> 2;
             size_t x = eb;
             const int e4 = x & 3; x >>= 2;
             const int ln = x & 63; x >>= 6;
@@ -721,6 +936,35 @@ __global__ void pack_kernel(PackArgs a, int l) {
             const int jj = frag_feature(o, r, hh);
             a.bp[a.bp_off[l] + ep] = (jj < N) ? a.B[(size_t)l * a.w_n + jj] : 0.0f;
         }
+    }
+}
+
+// bf16x6 planes: forward W6F[t][ks][o][p][lane][j] = plane p of W[f(t, 8ks+j, h)][32o + lane&31],
+// backward W6B[t][ks][o][p][lane][j] = plane p of W[32o + lane&31][f(t, 8ks+j, h)] (t = n tile).
+__global__ void pack6_kernel(PackArgs a, int l) {
+    const float* W = a.W + (size_t)l * a.w_k * a.w_n;
+    const int K = a.k[l], N = a.n[l];
+    const size_t nf = a.w6f_n[l], nb = a.w6b_n[l];
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < nf + nb;
+         e += (size_t)gridDim.x * blockDim.x) {
+        const bool fwd = e < nf;
+        size_t x = fwd ? e : e - nf;
+        const int no = fwd ? a.fo[l] : a.bo[l];
+        const int j = x & 7; x >>= 3;
+        const int ln = x & 63; x >>= 6;
+        const int pl = x % 3; x /= 3;
+        const int o = x % no; x /= no;
+        const int ks = x & 1; x >>= 1;
+        const int t = (int)x;
+        const int f = frag_feature(t, 8 * ks + j, ln >> 5), rr = 32 * o + (ln & 31);
+        const int kk = fwd ? f : rr, jj = fwd ? rr : f;
+        const float w = (kk < K && jj < N) ? W[(size_t)kk * a.w_n + jj] : 0.0f;
+        const __bf16 hi = (__bf16)w;
+        const float r = w - (float)hi;
+        const __bf16 mid = (__bf16)r;
+        const __bf16 lo = (__bf16)(r - (float)mid);
+        const __bf16 v = pl == 0 ? hi : (pl == 1 ? mid : lo);
+        a.w6[(fwd ? a.w6f_off[l] + e : a.w6b_off[l] + (e - nf))] = __builtin_bit_cast(unsigned short, v);
     }
 }
 
@@ -816,15 +1060,21 @@ __global__ void grad_reduce_kernel(ReduceArgs a) {
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 struct Layout {
+    int ht;                                   // hidden output tiles, rounded to 1/2/4/8
+    int fo[kMaxLayers], bo[kMaxLayers];       // output tiles of each layer's fwd / bwd MMA
     size_t wf_off[kMaxLayers], wb_off[kMaxLayers], bp_off[kMaxLayers];
     size_t wf_n[kMaxLayers], wb_n[kMaxLayers], bp_n[kMaxLayers];
     size_t pack_total;
+    size_t w6f_off[kMaxLayers], w6b_off[kMaxLayers], w6f_n[kMaxLayers], w6b_n[kMaxLayers];
+    size_t w6_total;                          // u16
     size_t act_off[kMaxLayers], x_off, act_total;
     size_t grad_off[kMaxLayers], grad_total;
     int splits[kMaxLayers], phases[kMaxLayers], mode[kMaxLayers], wg_off[kMaxLayers], dw_grid;
     size_t dwp_off[kMaxLayers], dwp_total, dbp_off[kMaxLayers], dbp_total;
     int num_wg, blocks, rpw;
 };
+
+inline int pow2_tiles(int t) { return t <= 1 ? 1 : t <= 2 ? 2 : t <= 4 ? 4 : 8; }
 
 void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S) {
     const int L = m.num_layers;
@@ -833,16 +1083,33 @@ void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S) {
         kt[l] = (m.k[l] + 31) / 32;
         nt[l] = (m.n[l] + 31) / 32;
     }
+    // the kernel runs every hidden layer's forward and every l >= 1 backward with HT output
+    // tiles, the head forward with 1 and the dX MMA with pow2(kt0): pack to exactly those
+    int mx = 1;
+    for (int l = 0; l + 1 < L; ++l) mx = nt[l] > mx ? nt[l] : mx;
+    y.ht = pow2_tiles(mx);
+    for (int l = 0; l < L; ++l) {
+        y.fo[l] = (l < L - 1) ? y.ht : 1;
+        y.bo[l] = (l >= 1) ? y.ht : pow2_tiles(kt[0]);
+    }
     size_t off = 0;
     for (int l = 0; l < L; ++l) {
-        y.wf_n[l] = (size_t)kt[l] * 16 * ((nt[l] + 3) / 4) * 256;
-        y.wb_n[l] = (size_t)nt[l] * 16 * ((kt[l] + 3) / 4) * 256;
+        y.wf_n[l] = (size_t)kt[l] * 16 * ((y.fo[l] + 3) / 4) * 256;
+        y.wb_n[l] = (size_t)nt[l] * 16 * ((y.bo[l] + 3) / 4) * 256;
         y.bp_n[l] = (size_t)nt[l] * 32;
         y.wf_off[l] = off; off += align_up(y.wf_n[l], 64);
         y.wb_off[l] = off; off += align_up(y.wb_n[l], 64);
         y.bp_off[l] = off; off += align_up(y.bp_n[l], 64);
     }
     y.pack_total = off;
+    off = 0;
+    for (int l = 0; l < L; ++l) {
+        y.w6f_n[l] = (size_t)kt[l] * 2 * y.fo[l] * 3 * 512;
+        y.w6b_n[l] = (size_t)nt[l] * 2 * y.bo[l] * 3 * 512;
+        y.w6f_off[l] = off; off += align_up(y.w6f_n[l], 512);
+        y.w6b_off[l] = off; off += align_up(y.w6b_n[l], 512);
+    }
+    y.w6_total = off;
     y.rpw = S >= kTileSamples ? 1 : kTileSamples / S;
     y.num_wg = (rays + y.rpw - 1) / y.rpw;
     y.blocks = y.num_wg * kWaves;
@@ -906,16 +1173,28 @@ bool fused_supported(const lnerf_mlp& m, int rays, int S, int input_mode, const 
 size_t fused_workspace_bytes(const lnerf_mlp& m, int rays, int S) {
     Layout y;
     make_layout(y, m, rays, S);
-    size_t f = align_up(y.pack_total, 64) + align_up(y.act_total, 64) + align_up(y.grad_total, 64) +
+    size_t f = align_up(y.pack_total, 64) + align_up((y.w6_total + 1) / 2, 64) +
+               align_up(y.act_total, 64) + align_up(y.grad_total, 64) +
                align_up((size_t)y.num_wg, 64) + align_up(y.dwp_total, 64) + align_up(y.dbp_total, 64) +
                64;
     return f * sizeof(float);
 }
 
-void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws_base) {
+void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws_base, int flags) {
     Layout y;
     make_layout(y, m, b.rays, b.samples);
     p.L = m.num_layers;
+    p.ht = y.ht;
+    // bf16x6 keeps (L-1)*HT ReLU-mask tiles in a smaller LDS budget (the ring is 1.5x larger)
+    p.x6 = !(flags & LNERF_MFMA_F32) && (p.L - 1) * y.ht <= kMaskTiles(true);
+    for (int l = 0; l < p.L; ++l) {
+        p.fo[l] = y.fo[l];
+        p.bo[l] = y.bo[l];
+        p.w6f_off[l] = y.w6f_off[l];
+        p.w6b_off[l] = y.w6b_off[l];
+        p.w6f_n[l] = y.w6f_n[l];
+        p.w6b_n[l] = y.w6b_n[l];
+    }
     for (int l = 0; l < p.L; ++l) {
         p.k[l] = m.k[l];
         p.n[l] = m.n[l];
@@ -950,6 +1229,8 @@ void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws
     p.wb = base + off;
     p.bp = base + off;
     off += align_up(y.pack_total, 64);
+    p.w6 = (unsigned short*)(base + off);
+    off += align_up((y.w6_total + 1) / 2, 64);
     p.act = base + off;
     off += align_up(y.act_total, 64);
     p.grad = base + off;
@@ -961,8 +1242,7 @@ void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws
     p.db_part = base + off;
     off += align_up(y.dbp_total, 64);
     p.loss_total = base + off;
-    // remember x slab offset in act_off[kMaxLayers-1] slot is not possible; keep it in a static
-    p.act_off[kMaxLayers - 1] = y.x_off;
+    p.x_off = y.x_off;
 }
 
 static void launch_pack(const FusedPlan& p, const float* ws, const float* bs, hipStream_t s) {
@@ -973,12 +1253,19 @@ static void launch_pack(const FusedPlan& p, const float* ws, const float* bs, hi
         a.n[l] = p.n[l];
         a.kt[l] = p.kt[l];
         a.nt[l] = p.nt[l];
+        a.fo[l] = p.fo[l];
+        a.bo[l] = p.bo[l];
         a.wf_off[l] = p.wf_off[l];
         a.wb_off[l] = p.wb_off[l];
         a.bp_off[l] = p.bp_off[l];
-        a.wf_n[l] = (size_t)p.kt[l] * 16 * ((p.nt[l] + 3) / 4) * 256;
-        a.wb_n[l] = (size_t)p.nt[l] * 16 * ((p.kt[l] + 3) / 4) * 256;
+        // the x6 path reads only the biases of the f32 region
+        a.wf_n[l] = p.x6 ? 0 : (size_t)p.kt[l] * 16 * ((p.fo[l] + 3) / 4) * 256;
+        a.wb_n[l] = p.x6 ? 0 : (size_t)p.nt[l] * 16 * ((p.bo[l] + 3) / 4) * 256;
         a.bp_n[l] = (size_t)p.nt[l] * 32;
+        a.w6f_off[l] = p.w6f_off[l];
+        a.w6b_off[l] = p.w6b_off[l];
+        a.w6f_n[l] = p.w6f_n[l];
+        a.w6b_n[l] = p.w6b_n[l];
     }
     a.w_k = p.w_k;
     a.w_n = p.w_n;
@@ -987,10 +1274,15 @@ static void launch_pack(const FusedPlan& p, const float* ws, const float* bs, hi
     a.wf = p.wf;
     a.wb = p.wb;
     a.bp = p.bp;
+    a.w6 = p.w6;
     for (int l = 0; l < p.L; ++l) {
+        if (p.x6) {
+            // biases (and nothing else) through pack_kernel: bp lands after wf_n + wb_n = 0
+            const size_t n6 = a.w6f_n[l] + a.w6b_n[l];
+            pack6_kernel<<<(unsigned)((n6 + 255) / 256), 256, 0, s>>>(a, l);
+        }
         const size_t n = a.wf_n[l] + a.wb_n[l] + a.bp_n[l];
-        unsigned g = (unsigned)((n + 255) / 256);
-        pack_kernel<<<g, 256, 0, s>>>(a, l);
+        pack_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(a, l);
     }
 }
 
@@ -1007,12 +1299,19 @@ static FusedArgs make_fused_args(const FusedPlan& p, const lnerf_batch& b, float
         a.act_off[l] = p.act_off[l];
         a.grad_off[l] = p.grad_off[l];
     }
+    if (p.x6) {
+        for (int l = 0; l < p.L; ++l) {
+            a.wf_off[l] = p.w6f_off[l];
+            a.wb_off[l] = p.w6b_off[l];
+        }
+    }
     a.k0 = p.k[0];
     a.wf = p.wf;
     a.wb = p.wb;
+    a.w6 = p.w6;
     a.bp = p.bp;
     a.act = p.act;
-    a.x_off = p.act_off[kMaxLayers - 1];
+    a.x_off = p.x_off;
     a.grad = p.grad;
     a.rays = p.rays;
     a.S = p.S;
@@ -1034,12 +1333,16 @@ static FusedArgs make_fused_args(const FusedPlan& p, const lnerf_batch& b, float
 }
 
 static void launch_fused(const FusedPlan& p, const FusedArgs& fa, hipStream_t s) {
-    int ht = 1;
-    for (int l = 0; l + 1 < p.L; ++l) ht = p.nt[l] > ht ? p.nt[l] : ht;
-    if (ht <= 1) fused_fwd_bwd_kernel<1><<<p.num_wg, kWgThreads, 0, s>>>(fa);
-    else if (ht <= 2) fused_fwd_bwd_kernel<2><<<p.num_wg, kWgThreads, 0, s>>>(fa);
-    else if (ht <= 4) fused_fwd_bwd_kernel<4><<<p.num_wg, kWgThreads, 0, s>>>(fa);
-    else fused_fwd_bwd_kernel<8><<<p.num_wg, kWgThreads, 0, s>>>(fa);
+#define LNERF_FUSED_LAUNCH(HT)                                                         \
+    if (p.x6) fused_fwd_bwd_kernel<HT, true><<<p.num_wg, kWgThreads, 0, s>>>(fa);      \
+    else fused_fwd_bwd_kernel<HT, false><<<p.num_wg, kWgThreads, 0, s>>>(fa);
+    switch (p.ht) {
+        case 1: LNERF_FUSED_LAUNCH(1) break;
+        case 2: LNERF_FUSED_LAUNCH(2) break;
+        case 4: LNERF_FUSED_LAUNCH(4) break;
+        default: LNERF_FUSED_LAUNCH(8) break;
+    }
+#undef LNERF_FUSED_LAUNCH
 }
 
 void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, const lnerf_batch& b,
@@ -1062,7 +1365,7 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
     for (int l = 0; l < p.L; ++l) {
         da.kt[l] = p.kt[l];
         da.nt[l] = p.nt[l];
-        da.a_off[l] = (l == 0) ? p.act_off[kMaxLayers - 1] : p.act_off[l - 1];
+        da.a_off[l] = (l == 0) ? p.x_off : p.act_off[l - 1];
         da.g_off[l] = p.grad_off[l];
         da.splits[l] = p.dw_splits[l];
         da.mode[l] = p.dw_mode[l];
@@ -1090,7 +1393,7 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
             ++da.nl;
         }
         da.wg_off[da.nl] = grid;
-        launch_dw(mode, grid, da, s);
+        launch_dw(mode, grid, da, p.x6 != 0, s);
     }
     mark(4);
     ReduceArgs ra{};

@@ -102,8 +102,14 @@ struct FusedPlan {
     float* wb;        // backward-packed weights
     float* bp;        // biases in fragment order
     size_t wf_off[kMaxLayers], wb_off[kMaxLayers], bp_off[kMaxLayers];
-    float* act;       // activation slabs: layer l at act_off[l] (l = -1 -> input X slab at x_off)
+    int ht;           // hidden output tiles (1/2/4/8): the fused kernel's instantiation
+    int x6;           // 1: bf16x6 split-plane MFMA; 0: exact f32 MFMA
+    int fo[kMaxLayers], bo[kMaxLayers];  // packed output tiles of each layer's fwd / bwd MMA
+    unsigned short* w6;                  // bf16x6 packed planes (u16 offsets below)
+    size_t w6f_off[kMaxLayers], w6b_off[kMaxLayers], w6f_n[kMaxLayers], w6b_n[kMaxLayers];
+    float* act;       // activation slabs: layer l at act_off[l], the input X slab at x_off
     size_t act_off[kMaxLayers];
+    size_t x_off;
     float* grad;      // gradient slabs G_l at grad_off[l]
     size_t grad_off[kMaxLayers];
     float* loss_part; // per-workgroup partial loss (num_wg)
@@ -121,7 +127,8 @@ struct FusedPlan {
 
 bool fused_supported(const lnerf_mlp& mlp, int rays, int S, int input_mode, const char** why);
 size_t fused_workspace_bytes(const lnerf_mlp& mlp, int rays, int S);
-void fused_plan(FusedPlan& p, const lnerf_mlp& mlp, const lnerf_batch& b, void* ws_base);
+// flags: LNERF_MFMA_F32 selects the exact f32 MFMA products over the default bf16x6 split
+void fused_plan(FusedPlan& p, const lnerf_mlp& mlp, const lnerf_batch& b, void* ws_base, int flags);
 // ev: nullable array of 7 events recorded between the step's kernels (LNERF_TIMING)
 void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, const lnerf_batch& b,
                       float seed, int flags, const lnerf_outputs& out, hipStream_t s,

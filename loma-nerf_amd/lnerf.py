@@ -26,6 +26,7 @@ WANT_DX = 4
 GENERIC = 8
 FAST = 16
 TIMING = 32
+MFMA_F32 = 64     # fused path: exact f32 MFMA instead of the bf16x6 split
 
 # every symbol include/lnerf.h declares (tests check the library exports all of them)
 EXPORTED_SYMBOLS = [

@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Accuracy of each step implementation against the float64 numpy restatement (oracle/nerf_np.py)
+on a cfg3 subset (the bench MLP 33->256x7->4, 64 samples): the C loma-order fp32 oracle, the
+generic device path, the fused path with exact f32 MFMA and with the bf16x6 split. Test/report
+infrastructure (imports the oracle); writes gpurun_out/precision.json.
+
+    python scripts/precision_report.py [--rays 64]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+for p in ("oracle", "loma-nerf_amd", "tests"):
+    sys.path.insert(0, os.path.join(REPO, p))
+
+
+def errors(got, ref):
+    out = {}
+    for k in ("acc", "dW", "dB", "d_dists", "d_target"):
+        g = np.asarray(got[k], np.float64)
+        r = np.asarray(ref[k], np.float64)
+        scale = np.abs(r).max()
+        big = np.abs(r) > 1e-3 * scale
+        out[k] = {"max_abs_over_max": float(np.abs(g - r).max() / scale),
+                  "median_rel": float(np.median(np.abs(g - r)[big] / np.abs(r)[big])),
+                  "p99_rel": float(np.percentile(np.abs(g - r)[big] / np.abs(r)[big], 99))}
+    out["loss_rel"] = float(abs(got["loss"] - ref["loss"]) / abs(ref["loss"]))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rays", type=int, default=64)
+    args = ap.parse_args()
+    import lnerf
+    import nerf_np
+    import oracle
+    from test_gpu_native import oracle_ref, run_native
+
+    w = nerf_np.make_workload("cfg3", rays=args.rays)
+    X64 = nerf_np.positional_encoding_3d(w.pts32.astype(np.float64), w.F).reshape(w.X.shape)
+    ref = nerf_np.nerf_forward_backward(X64, [x.astype(np.float64) for x in w.ws],
+                                        [x.astype(np.float64) for x in w.bs], w.dists, w.target,
+                                        w.S, seed=1.0)
+    L = len(w.ws)
+    dW = np.zeros(w.wp.shape)
+    dB = np.zeros(w.bp.shape)
+    for l in range(L):
+        k, n = w.ws[l].shape
+        dW[l, :k, :n] = ref["dW"][l]
+        dB[l, :n] = ref["db"][l]
+    ref = dict(loss=ref["loss"], acc=ref["acc"], dW=dW, dB=dB, d_dists=ref["d_dists"],
+               d_target=ref["d_target"])
+
+    eng = lnerf.Engine(0)
+    rep = {"workload": f"cfg3 subset: {args.rays} rays x {w.S} samples, MLP 33->256x7->4, seed 1",
+           "reference": "float64 numpy restatement (oracle/nerf_np.py)"}
+    rep["oracle_c_fp32"] = errors(oracle_ref(w, seed=1.0), ref)
+    rep["generic_device"] = errors(run_native(eng, w, seed=1.0, flags=lnerf.GENERIC), ref)
+    rep["fused_f32_mfma"] = errors(run_native(eng, w, seed=1.0, flags=lnerf.FAST | lnerf.MFMA_F32), ref)
+    rep["fused_bf16x6"] = errors(run_native(eng, w, seed=1.0, flags=lnerf.FAST), ref)
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(REPO, "gpurun_out", "precision.json"), "w") as fh:
+        json.dump(rep, fh, indent=1)
+    for k, v in rep.items():
+        if isinstance(v, dict):
+            print(k, {kk: (vv["max_abs_over_max"] if isinstance(vv, dict) else vv)
+                      for kk, vv in v.items()})
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -4,7 +4,8 @@ size-independent properties at the full bench size (4096 rays x 64 samples, 8x25
 Tolerance (fp32, north_star "within 1e-4"): |got - want| <= 1e-4 |want| + 1e-4 max|want| per
 tensor. The fused path sums in a different order than the scalar loma-order oracle (MFMA k-order,
 split-K over samples), so it is not bit-exact; sample/ray indexing is exact by construction
-(tested with per-ray outputs).
+(tested with per-ray outputs). Both fused precisions are checked: the default bf16x6 split
+(fp32-accurate products on the bf16 MFMA) and the exact f32 MFMA (LNERF_MFMA_F32).
 """
 import numpy as np
 import pytest
@@ -59,19 +60,44 @@ def compare(got, want, keys=("dW", "dB", "d_dists", "d_target"), tol=TOL):
         assert_close(k, got[k], want[k], **tol)
 
 
+PRECISIONS = [0, 64]   # default bf16x6 split, lnerf.MFMA_F32
+
+
+@pytest.mark.parametrize("prec", PRECISIONS)
 @pytest.mark.parametrize("points", [True, False])
-def test_fused_cfg2_matches_oracle(engine, points):
+def test_fused_cfg2_matches_oracle(engine, points, prec):
     """Config 2 (train_nerf-sized MLP 33->30->30->4), 1024 rays x 32 samples, seed = loss."""
     w = nerf_np.make_workload("cfg2")
-    got = run_native(engine, w, points=points)
+    got = run_native(engine, w, points=points, flags=prec)
     want = oracle_ref(w, points=points)
     compare(got, want)
 
 
-def test_fused_cfg3_subset_matches_oracle(engine):
+@pytest.mark.parametrize("prec", PRECISIONS)
+def test_fused_cfg3_subset_matches_oracle(engine, prec):
     """The bench MLP (33->256x7->4) on 24 rays x 64 samples, seed = loss."""
     w = nerf_np.make_workload("cfg3", rays=24)
-    got = run_native(engine, w)
+    got = run_native(engine, w, flags=prec)
+    want = oracle_ref(w)
+    compare(got, want)
+
+
+@pytest.mark.parametrize("prec", PRECISIONS)
+def test_fused_nonuniform_widths(engine, prec):
+    """Hidden widths that differ per layer (33->128->256->64->100->4): every layer's MMA runs
+    with the widest layer's tile count over zero-padded packed weights."""
+    w = nerf_np.make_workload("cfg2", rays=40, samples=48)
+    rng = np.random.RandomState(3)
+    dims = [33, 128, 256, 64, 100, 4]
+    ws = [(rng.randn(k, n) * np.sqrt(2.0 / k)).astype(np.float32) for k, n in zip(dims, dims[1:])]
+    bs = [(rng.randn(n) * 0.5).astype(np.float32) for n in dims[1:]]
+    wp = np.zeros((len(ws), 256, 256), np.float32)
+    bp = np.zeros((len(ws), 256), np.float32)
+    for l, (a, b) in enumerate(zip(ws, bs)):
+        wp[l, :a.shape[0], :a.shape[1]] = a
+        bp[l, :b.shape[0]] = b
+    w = nerf_np.Workload(w.pts, w.pts32, w.X, w.dists, w.target, ws, bs, wp, bp, w.F, w.S, w.N)
+    got = run_native(engine, w, flags=prec)
     want = oracle_ref(w)
     compare(got, want)
 
@@ -170,8 +196,9 @@ def test_full_size_oracle_rays_spotcheck(engine, full):
 
 # ---- against the committed golden fixtures (float64 numpy restatement) ------------------------
 
+@pytest.mark.parametrize("prec", PRECISIONS)
 @pytest.mark.parametrize("name", ["chunk_4x30.npz", "deep8_w64_2x64.npz", "trained_weights_8x16.npz"])
-def test_fused_matches_golden_fixture(engine, name):
+def test_fused_matches_golden_fixture(engine, name, prec):
     import os
     import lnerf
     import torch
@@ -183,7 +210,7 @@ def test_fused_matches_golden_fixture(engine, name):
     d = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to("cuda:0")
     r = engine.train_step(mlp, d(g["wp"]), d(g["bp"]), d(g["X"]), d(g["dists"]), d(g["target"]),
                           samples=S, input_mode=lnerf.INPUT_ENCODED, seed=1.0, want_per_ray=True,
-                          want_dx=True, flags=lnerf.FAST)
+                          want_dx=True, flags=lnerf.FAST | prec)
     torch.cuda.synchronize()
     assert abs(float(r.loss.item()) - g["loss"]) <= 1e-5 * abs(g["loss"])
     assert_close("acc", r.acc_color.cpu().numpy(), g["acc"], **TOL)

@@ -231,6 +231,92 @@ __device__ __forceinline__ fx16 mfma_x6(const bf8& wh, const bf8& wm, const bf8&
 // [s][o][p][lane][8 x bf16], the 8 k's of lane half h being the features that accumulator
 // registers 8s..8s+7 of the input tile hold (cdna_hip_programming.md "accumulator tile as the
 // next MFMA's operand"). The B operand is the input tile itself, split into planes on the fly.
+// LDS byte address of a generic pointer into __shared__ memory.
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+    return (unsigned)(size_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// ds_read_b128 outside the compiler's waitcnt bookkeeping (paired with lgkm_wait_for).
+template <int OFF>
+__device__ __forceinline__ bf8 ds_read_b128_at(unsigned addr) {
+    bf8 r;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+    return r;
+}
+
+// s_waitcnt lgkmcnt(N) that the three fragments depend on (so no use can be scheduled above it).
+template <int N>
+__device__ __forceinline__ void lgkm_wait_for(bf8& a, bf8& b, bf8& c) {
+    asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(a), "+v"(b), "+v"(c) : "n"(N));
+}
+
+// The fragment-read / MFMA pipeline of one staged chunk, unrolled at compile time (the LDS
+// offsets are instruction immediates): reads of steps 0 and 1 first, then per step I the reads
+// of step I+2, a wait that leaves those (and step I+1's) in flight, and step I's six MFMAs.
+template <int NS>
+__device__ __forceinline__ void x6_prologue(unsigned base, bf8 (&w)[NS][3]) {
+    w[0][0] = ds_read_b128_at<0 * 1024>(base);
+    w[0][1] = ds_read_b128_at<1 * 1024>(base);
+    w[0][2] = ds_read_b128_at<2 * 1024>(base);
+    if constexpr (NS > 1) {
+        w[1][0] = ds_read_b128_at<3 * 1024>(base);
+        w[1][1] = ds_read_b128_at<4 * 1024>(base);
+        w[1][2] = ds_read_b128_at<5 * 1024>(base);
+    }
+}
+
+// A slab tile store spread over the step pipeline: its LDS transpose writes at step 0, the
+// transposed reads half way, the global stores at the last step, so neither LDS round trip
+// stalls the MFMA stream.
+struct TileStore {
+    const fx16* v;   // accumulator-layout tile (nullptr: nothing to store)
+    float* dst;      // [32 features][32 samples] slab block
+    float* tr;       // this wave's 32x32 LDS transpose tile
+    fx4 t[4];
+};
+
+__device__ __forceinline__ void tile_store_write(TileStore& ts) {
+    if (!ts.v) return;
+    const int lane = threadIdx.x & 63, h = lane >> 5, sl = lane & 31;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) ts.tr[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + sl] = (*ts.v)[r];
+}
+
+__device__ __forceinline__ void tile_store_read(TileStore& ts) {
+    if (!ts.v) return;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ts.t[q] = *(const fx4*)(ts.tr + ((lane >> 3) + 8 * q) * 32 + (lane & 7) * 4);
+}
+
+__device__ __forceinline__ void tile_store_global(TileStore& ts) {
+    if (!ts.v) return;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        __builtin_nontemporal_store(ts.t[q], (fx4*)(ts.dst + ((lane >> 3) + 8 * q) * 32 + (lane & 7) * 4));
+}
+
+template <int NS, int NTO, int I>
+__device__ __forceinline__ void x6_step(unsigned base, bf8 (&w)[NS][3], const bf8 (&bp)[2][3],
+                                        fx16 (&out)[kNT], TileStore& ts) {
+    if constexpr (I < NS) {
+        if constexpr (I + 2 < NS) {
+            w[I + 2][0] = ds_read_b128_at<((I + 2) * 3 + 0) * 1024>(base);
+            w[I + 2][1] = ds_read_b128_at<((I + 2) * 3 + 1) * 1024>(base);
+            w[I + 2][2] = ds_read_b128_at<((I + 2) * 3 + 2) * 1024>(base);
+        }
+        if constexpr (I == 0) tile_store_write(ts);
+        if constexpr (I == NS / 2) tile_store_read(ts);
+        if constexpr (I == NS - 1) tile_store_global(ts);
+        lgkm_wait_for<(I + 2 < NS ? 6 : (I + 1 < NS ? 3 : 0))>(w[I][0], w[I][1], w[I][2]);
+        constexpr int ks = I / NTO, o = I % NTO;
+        out[o] = mfma_x6(w[I][0], w[I][1], w[I][2], bp[ks][0], bp[ks][1], bp[ks][2], out[o]);
+        __builtin_amdgcn_sched_barrier(0);
+        x6_step<NS, NTO, I + 1>(base, w, bp, out, ts);
+    }
+}
+
 template <int NTO>
 __device__ __forceinline__ void mma_stream_x6(const unsigned short* __restrict__ src, int nchunks,
                                               const fx16 (&in)[kNT], fx16 (&out)[kNT],
@@ -250,40 +336,26 @@ __device__ __forceinline__ void mma_stream_x6(const unsigned short* __restrict__
             const unsigned char* cur = ring + (c & 1) * SLOT + lane * 16;
             if (c + 1 < nchunks)
                 stage_bytes_t<CB>((const char*)src + (size_t)(c + 1) * CB, ring + ((c + 1) & 1) * SLOT);
-            if (tstore && c >= 1) store_tile(in[c - 1], tstore + (c - 1) * 1024, tr);
+            TileStore tsx;
+            tsx.v = (tstore && c >= 1) ? &in[c - 1] : nullptr;
+            tsx.dst = tstore + (c - 1) * 1024;
+            tsx.tr = tr;
             // retire any scalar (kernarg) loads still in flight: while one is pending the
             // waitcnt pass can only emit lgkmcnt(0) for the LDS fragment reads below
             __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0), vmcnt/expcnt untouched
             __builtin_amdgcn_sched_barrier(0);
             // software-pipelined two steps deep: the three planes of step i+2 are read while
-            // step i's six MFMAs run, so a step's fragments have had a whole step to land
+            // step i's six MFMAs run. The fragment reads are inline asm with an explicit,
+            // dependency-carrying lgkmcnt(N) before each step's MFMAs: the compiler's own waitcnt
+            // insertion emits lgkmcnt(0) here, which also waits for the reads just issued.
             constexpr int NS = 2 * NTO;
+            const unsigned base = lds_addr(cur);
             bf8 bp[2][3];
-            split3(in[c], 0, bp[0][0], bp[0][1], bp[0][2]);
             bf8 w[NS][3];
-#pragma unroll
-            for (int i = 0; i < 2 && i < NS; ++i)
-#pragma unroll
-                for (int pl = 0; pl < 3; ++pl) w[i][pl] = *(const bf8*)(cur + (i * 3 + pl) * 1024);
-#pragma unroll
-            for (int i = 0; i < NS; ++i) {
-                const int ks = i / NTO, o = i % NTO;
-                if (i + 2 < NS) {
-#pragma unroll
-                    for (int pl = 0; pl < 3; ++pl)
-                        w[i + 2][pl] = *(const bf8*)(cur + ((i + 2) * 3 + pl) * 1024);
-                }
-                if (i == 0) split3(in[c], 1, bp[1][0], bp[1][1], bp[1][2]);
-                out[o] = mfma_x6(w[i][0], w[i][1], w[i][2], bp[ks][0], bp[ks][1], bp[ks][2], out[o]);
-            }
-            // pin that order for the scheduler: [reads of steps 0, 1], then per step i the
-            // reads of step i+2 followed by the six MFMAs of step i
-            __builtin_amdgcn_sched_group_barrier(0x100, NS >= 2 ? 6 : 3, 0);
-#pragma unroll
-            for (int i = 0; i < NS; ++i) {
-                if (i + 2 < NS) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
-            }
+            x6_prologue<NS>(base, w);
+            split3(in[c], 0, bp[0][0], bp[0][1], bp[0][2]);
+            split3(in[c], 1, bp[1][0], bp[1][1], bp[1][2]);
+            x6_step<NS, NTO, 0>(base, w, bp, out, tsx);
             dma_barrier();
             if (tstore && c == nchunks - 1) store_tile(in[c], tstore + c * 1024, tr);
         }
@@ -513,26 +585,58 @@ __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs 
 
     fx16 act[kNT], out[kNT];
     // ---- layer-0 input: features in accumulator order ----
-    // Each 32-feature tile is produced into a per-wave LDS scratch (the weight ring is free
-    // before the first layer) by a compact loop, then picked up in accumulator order.
-    float* pe = ldsw + (size_t)wave * (32 * 33);
+    // Produced into a per-wave LDS scratch (the weight ring is free before the first layer),
+    // then picked up in accumulator order. POINTS mode with 3 + 6F <= 64 (F <= 10) computes
+    // each (sample, coordinate, frequency) once with a float64 sincos (pos_encoding.py:54-66:
+    // f64 trig of the point, rounded to f32 once); other inputs go tile by tile.
     const int tile_base = wg * tile_samples + wave * 32;
 #pragma unroll
-    for (int t = 0; t < kNT; ++t) {
+    for (int t = 0; t < kNT; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) act[t][r] = 0.0f;
-        if (t < a.kt[0]) {
-            for (int e = lane; e < 32 * 32; e += 64) {
-                const int sl = e >> 5, ft = e & 31;
-                const int lsl = wave * 32 + sl;
-                const bool vs = (lsl < tile_samples) && (tile_base + sl < a.R);
-                pe[sl * 33 + ft] = input_feature(a, tile_base + sl, vs, 32 * t + ft);
+    if (a.input_mode == LNERF_INPUT_POINTS && a.k0 <= 64) {
+        constexpr int kStride = 65;
+        float* pe = ldsw + (size_t)wave * (32 * kStride);
+        const int F = a.F, per = 3 * (F + 1);
+        for (int it = lane; it < 32 * per; it += 64) {
+            const int sl = it / per, rem = it - sl * per, c = rem % 3, q = rem / 3;
+            const bool vs = (wave * 32 + sl < tile_samples) && (tile_base + sl < a.R);
+            const float xc = vs ? a.x[(size_t)(tile_base + sl) * 3 + c] : 0.0f;
+            if (q == 0) {
+                pe[sl * kStride + c] = xc;
+            } else {
+                double sn, cs;
+                sincos(ldexp((double)xc, q - 1), &sn, &cs);
+                pe[sl * kStride + 3 + 6 * (q - 1) + c] = (float)sn;
+                pe[sl * kStride + 6 + 6 * (q - 1) + c] = (float)cs;
             }
-            __syncthreads();
-#pragma unroll
-            for (int r = 0; r < 16; ++r) act[t][r] = pe[(lane & 31) * 33 + (frag_feature(t, r, h) - 32 * t)];
-            __syncthreads();
         }
+        for (int e = lane; e < 32 * 64; e += 64) {        // zero the padded features
+            const int sl = e >> 6, f = e & 63;
+            if (f >= a.k0) pe[sl * kStride + f] = 0.0f;
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+            if (t < a.kt[0]) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) act[t][r] = pe[(lane & 31) * kStride + frag_feature(t, r, h)];
+            }
+        __syncthreads();   // the ring DMA of layer 0 overwrites the scratch
+    } else {
+        float* pe = ldsw + (size_t)wave * (32 * 33);
+#pragma unroll
+        for (int t = 0; t < kNT; ++t) {
+            if (t < a.kt[0]) {
+                for (int e = lane; e < 32 * 32; e += 64) {
+                    const int sl = e >> 5, ft = e & 31;
+                    const bool vs = (wave * 32 + sl < tile_samples) && (tile_base + sl < a.R);
+                    pe[sl * 33 + ft] = input_feature(a, tile_base + sl, vs, 32 * t + ft);
+                }
+#pragma unroll
+                for (int r = 0; r < 16; ++r) act[t][r] = pe[(lane & 31) * 33 + (frag_feature(t, r, h) - 32 * t)];
+            }
+        }
+        __syncthreads();
     }
 
     // ---- forward through the layers ----

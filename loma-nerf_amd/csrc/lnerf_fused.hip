@@ -125,6 +125,12 @@ __device__ __forceinline__ void dma_barrier_n() {
 }
 __device__ __forceinline__ void dma_barrier() { dma_barrier_n<0>(); }
 
+// Offset of (feature row, sample) inside a 4-KiB slab tile: two halves of 16 samples, each
+// [32 rows][16 samples], so the dW kernel streams a 16-sample half-block as contiguous 2-KiB runs.
+__host__ __device__ __forceinline__ int slab_off(int row, int sample) {
+    return (sample >> 4) * 512 + row * 16 + (sample & 15);
+}
+
 // Store one 32x32 accumulator tile (lane = sample, registers = features in C/D order) as a
 // row-major [feature][32 samples] block: transpose through the wave's LDS tile, then 4
 // global_store_dwordx4 per lane (each wave instruction writes 8 whole 128-B rows).
@@ -137,7 +143,7 @@ __device__ __forceinline__ void store_tile(const fx16& v, float* __restrict__ ds
         const int row = (lane >> 3) + 8 * q, c4 = (lane & 7) * 4;
         const fx4 x = *(const fx4*)(tr + row * 32 + c4);
         // streaming store (nt): the slabs are read once, by the dW kernel; keep L2 for weights
-        __builtin_nontemporal_store(x, (fx4*)(dst + row * 32 + c4));
+        __builtin_nontemporal_store(x, (fx4*)(dst + slab_off(row, c4)));
     }
 }
 
@@ -294,7 +300,7 @@ __device__ __forceinline__ void tile_store_global(TileStore& ts) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-        __builtin_nontemporal_store(ts.t[q], (fx4*)(ts.dst + ((lane >> 3) + 8 * q) * 32 + (lane & 7) * 4));
+        __builtin_nontemporal_store(ts.t[q], (fx4*)(ts.dst + slab_off((lane >> 3) + 8 * q, (lane & 7) * 4)));
 }
 
 template <int NS, int NTO, int I>
@@ -785,7 +791,7 @@ __device__ __forceinline__ void dw_stage(const float* __restrict__ src, float* d
     for (int i = wave; i < rows / 8; i += kWaves) {
         const int row = i * 8 + (lane >> 3);
         const int c = swz_chunk(row, lane & 7);
-        const float* g = src + row * 32 + c * 4;
+        const float* g = src + (row >> 5) * 1024 + slab_off(row & 31, c * 4);
         float* l = dst + i * 256;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                          (__attribute__((address_space(3))) void*)l, 16, 0, 0);
@@ -953,28 +959,27 @@ __device__ __forceinline__ void dw_run(const DwArgs a, int l, int sp, float* lds
 #define LNERF_DW_PHASED_SHAPES(X) X(1, 1, 1) X(2, 1, 2) X(1, 2, 3) X(2, 2, 4) X(2, 4, 5) X(4, 2, 6) \
     X(2, 8, 7) X(8, 1, 8) X(4, 1, 9) X(1, 4, 10) X(8, 2, 11) X(1, 8, 12) X(4, 4, 13)
 
-// One launch per group of layers sharing an instantiation (all blocked layers together, each
-// phased shape on its own), so no kernel merges different accumulator sets.
-// X6: bf16x6 products (blocked layers only; the small phased layers stay on f32 MFMA).
-template <int TI, int TJ, bool PHASED, bool X6>
-__global__ void __launch_bounds__(kWgThreads, 1) dw_kernel(DwArgs a) {
+// Every layer in ONE launch (each workgroup's layer picks its instantiation), so the small
+// phased layers fill the machine beside the blocked ones instead of running after them; the
+// per-layer splits are balanced by slab bytes (make_layout).
+template <bool X6>
+__global__ void __launch_bounds__(kWgThreads, 1) dw_all_kernel(DwArgs a) {
     __shared__ __attribute__((aligned(16))) float lds[2 * kDwStageFloats];
     int i = 0;
     while (i + 1 < a.nl && (int)blockIdx.x >= a.wg_off[i + 1]) ++i;
-    dw_run<TI, TJ, PHASED, X6>(a, a.lid[i], blockIdx.x - a.wg_off[i], lds);
+    const int l = a.lid[i], sp = blockIdx.x - a.wg_off[i];
+    switch (a.mode[l]) {
+#define LNERF_DW_ALL_CASE(I, J, M) \
+    case M: dw_run<I, J, true, false>(a, l, sp, lds); break;
+        LNERF_DW_PHASED_SHAPES(LNERF_DW_ALL_CASE)
+#undef LNERF_DW_ALL_CASE
+        default: dw_run<4, 4, false, X6>(a, l, sp, lds); break;
+    }
 }
 
-void launch_dw(int mode, int grid, const DwArgs& a, bool x6, hipStream_t s) {
-    switch (mode) {
-#define LNERF_DW_CASE(I, J, M) \
-    case M: dw_kernel<I, J, true, false><<<grid, kWgThreads, 0, s>>>(a); break;
-        LNERF_DW_PHASED_SHAPES(LNERF_DW_CASE)
-#undef LNERF_DW_CASE
-        default:
-            if (x6) dw_kernel<4, 4, false, true><<<grid, kWgThreads, 0, s>>>(a);
-            else dw_kernel<4, 4, false, false><<<grid, kWgThreads, 0, s>>>(a);
-            break;
-    }
+void launch_dw_all(int grid, const DwArgs& a, bool x6, hipStream_t s) {
+    if (x6) dw_all_kernel<true><<<grid, kWgThreads, 0, s>>>(a);
+    else dw_all_kernel<false><<<grid, kWgThreads, 0, s>>>(a);
 }
 
 int dw_mode_for(int kt, int nt) {
@@ -1224,18 +1229,20 @@ void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S) {
     off = 0;
     for (int l = 0; l < L; ++l) { y.grad_off[l] = off; off += (size_t)y.blocks * nt[l] * 1024; }
     y.grad_total = off;
-    // dW launches: one per instantiation group (blocked layers together; each phased small-layer
-    // shape alone). A blocked group spreads ~256 workgroups over its layers (1 per CU: 128 KiB
-    // of LDS); a phased layer costs ~1/4..1/16 of a blocked one per slab and gets 128.
+    // dW: one launch over every layer (dw_all_kernel), ~kDwGrid workgroups split between the
+    // layers in proportion to the slab bytes each one streams (kt + nt tiles per 32-sample
+    // block): the kernel is bandwidth-bound, so equal bytes per workgroup balance it. Phased
+    // (small) layers write 4 partials per split.
+    constexpr int kDwGrid = 512;
     size_t dwp = 0, dbp = 0;
-    int nblocked = 0;
+    int tiles_sum = 0;
     for (int l = 0; l < L; ++l) {
         y.mode[l] = dw_mode_for(kt[l], nt[l]);
-        if (!y.mode[l]) ++nblocked;
+        tiles_sum += kt[l] + nt[l];
     }
     int wg = 0;
     for (int l = 0; l < L; ++l) {
-        int sp = y.mode[l] ? 128 : 256 / (nblocked ? nblocked : 1);
+        int sp = (int)((long long)kDwGrid * (kt[l] + nt[l]) / tiles_sum);
         sp = sp < 1 ? 1 : sp;
         sp = sp > y.blocks ? y.blocks : sp;
         y.splits[l] = sp;
@@ -1481,24 +1488,13 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
     da.blocks = p.blocks;
     da.dw_part = p.dw_part;
     da.db_part = p.db_part;
-    // one launch per instantiation group
-    bool done[kMaxLayers] = {};
-    for (int l0 = 0; l0 < p.L; ++l0) {
-        if (done[l0]) continue;
-        const int mode = p.dw_mode[l0];
-        da.nl = 0;
-        int grid = 0;
-        for (int l = l0; l < p.L; ++l) {
-            if (done[l] || p.dw_mode[l] != mode) continue;
-            done[l] = true;
-            da.lid[da.nl] = l;
-            da.wg_off[da.nl] = grid;
-            grid += p.dw_splits[l];
-            ++da.nl;
-        }
-        da.wg_off[da.nl] = grid;
-        launch_dw(mode, grid, da, p.x6 != 0, s);
+    da.nl = p.L;
+    for (int l = 0; l < p.L; ++l) {
+        da.lid[l] = l;
+        da.wg_off[l] = p.dw_split_off[l];
     }
+    da.wg_off[p.L] = p.dw_grid;
+    launch_dw_all(p.dw_grid, da, p.x6 != 0, s);
     mark(4);
     ReduceArgs ra{};
     ra.L = p.L;

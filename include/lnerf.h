@@ -11,9 +11,9 @@
  *
  *  (2) the native batched API on device-resident, contiguous buffers (the throughput path).
  *
- * No torch or HIP types appear here: streams are passed as `void*` (a hipStream_t, NULL = the
- * calling thread's default engine stream). Every entry point returns 0 on success / a negative
- * error code, or (loma-compat float returns) NaN on failure; lnerf_last_error() describes it.
+ * No torch or HIP types appear here: streams are passed as `void*` (a hipStream_t; NULL = the
+ * device's default (null) stream, which is torch's default stream). Every entry point returns 0
+ * on success / a negative error code, or (loma-compat float returns) NaN on failure; lnerf_last_error() describes it.
  */
 #ifndef LNERF_H
 #define LNERF_H
@@ -100,8 +100,12 @@ typedef struct {
 
 enum {
     LNERF_INPUT_ENCODED = 0, /* x = layer_input, (rays*S, k[0]) float32 row-major          */
-    LNERF_INPUT_POINTS = 1   /* x = sample positions, (rays*S, 3) float32; the engine      */
+    LNERF_INPUT_POINTS = 1,  /* x = sample positions, (rays*S, 3) float32; the engine      */
                              /*     applies positional_encoding_3d (pos_encoding.py:38-69)  */
+    LNERF_INPUT_RAYS = 2     /* x = rays, (rays, 6) float32 [origin xyz, direction xyz]; the */
+                             /*     engine samples t = linspace(near, far, S), the points   */
+                             /*     o + d t and dists = [diff(t), 1e8] in float64           */
+                             /*     (train_nerf.py:289-306), then applies the encoding      */
 };
 
 /* One batch of rays; all pointers are device pointers. Sample r of ray i is row i*S + r
@@ -112,8 +116,10 @@ typedef struct {
     int input_mode;      /* LNERF_INPUT_* */
     int num_freqs;       /* F (POINTS mode; k[0] must equal 3 + 6F) */
     const float* x;
-    const float* dists;  /* (rays, S) delta t, last = 1e8 in the reference (train_nerf.py:306) */
+    const float* dists;  /* (rays, S) delta t, last = 1e8 in the reference (train_nerf.py:306); */
+                         /* ignored (may be NULL) in RAYS mode                               */
     const float* target; /* (rays, 3) */
+    float near_t, far_t; /* RAYS mode: sampling range (train_nerf.py: near 2, far 6)          */
 } lnerf_batch;
 
 enum {
@@ -153,6 +159,13 @@ size_t lnerf_workspace_bytes(const lnerf_mlp* mlp, int rays, int samples);
 int lnerf_train_step(lnerf_ctx* ctx, const lnerf_mlp* mlp, const float* ws, const float* bs,
                      const lnerf_batch* batch, float seed, int flags, const lnerf_outputs* out,
                      void* stream);
+
+/* get_rays (train_nerf.py:23-62) on the device: the width x width pixel grid of
+ * linspace(0, 1, width) (the reference uses `width` for both axes), directions
+ * [(i - K[0][2]) / K[0][0], -(j - K[1][2]) / K[1][1], -1] rotated by c2w[:3,:3], origins
+ * c2w[:3,3], computed in float64 and stored as float32 rays (width*width, 6) = [o, d], ready for
+ * LNERF_INPUT_RAYS. K (3x3) and c2w (3x4 or the top of a 4x4, row-major) are host arrays. */
+int lnerf_get_rays(int width, const double* K, const double* c2w, float* rays, void* stream);
 
 /* Forward only (eval render, train_nerf.py:616-661): acc_color and, if target != NULL, loss. */
 int lnerf_render(lnerf_ctx* ctx, const lnerf_mlp* mlp, const float* ws, const float* bs,

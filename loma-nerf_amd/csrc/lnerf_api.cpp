@@ -626,12 +626,14 @@ static void validate(const lnerf_mlp* m, const lnerf_batch* b) {
     }
     if (m->n[m->num_layers - 1] < 4) fail("head needs >= 4 outputs");
     if (b->rays < 1 || b->samples < 1) fail("empty batch");
-    if (!b->x || !b->dists || !b->target) fail("null batch pointer");
-    if (b->input_mode == LNERF_INPUT_POINTS) {
-        if (m->k[0] != 3 + 6 * b->num_freqs) fail("POINTS mode needs k[0] == 3 + 6F");
+    if (!b->x || !b->target) fail("null batch pointer");
+    if (b->input_mode == LNERF_INPUT_POINTS || b->input_mode == LNERF_INPUT_RAYS) {
+        if (b->num_freqs < 0 || m->k[0] != 3 + 6 * b->num_freqs)
+            fail("POINTS/RAYS mode needs k[0] == 3 + 6F");
     } else if (b->input_mode != LNERF_INPUT_ENCODED) {
         fail("unknown input_mode");
     }
+    if (b->input_mode != LNERF_INPUT_RAYS && !b->dists) fail("null dists");
 }
 
 extern "C" size_t lnerf_workspace_bytes(const lnerf_mlp* mlp, int rays, int samples) {
@@ -678,12 +680,20 @@ static void generic_step(lnerf_ctx* ctx, const lnerf_mlp& m, const float* ws, co
                  odrg = k.take(nS * 4), odal = k.take(nS), odcp = k.take(nS), odws = k.take(nS),
                  odd = k.take(nS), odacc = k.take((size_t)th * 3), odT = k.take((size_t)th * 3),
                  odW = k.take((size_t)L * m.w_k * m.w_n), odB = k.take((size_t)L * m.w_n),
-                 oloss = k.take(1), oseed = k.take(1), odX = k.take((size_t)R * m.k[0]);
+                 oloss = k.take(1), oseed = k.take(1), odX = k.take((size_t)R * m.k[0]),
+                 odist = k.take(nS);
     float* g = (float*)ctx->generic_ws.get(k.off * sizeof(float));
     const float* X = bt.x;
+    const float* dists = bt.dists;
     if (bt.input_mode == LNERF_INPUT_POINTS) {
         k_positional_encoding(bt.x, R, bt.num_freqs, g + oX, m.k[0], s);
         X = g + oX;
+    } else if (bt.input_mode == LNERF_INPUT_RAYS) {
+        k_positional_encoding_rays(bt.x, bt.rays, S, bt.near_t, bt.far_t, bt.num_freqs, g + oX,
+                                   m.k[0], s);
+        k_ray_dists(bt.rays, S, bt.near_t, bt.far_t, g + odist, s);
+        X = g + oX;
+        dists = g + odist;
     }
     // forward call (nerf_evaluate_and_march)
     HIP_OK(hipMemsetAsync(g + oIO, 0, nio * sizeof(float), s));
@@ -695,7 +705,7 @@ static void generic_step(lnerf_ctx* ctx, const lnerf_mlp& m, const float* ws, co
     b.T = bt.target;
     b.IO = g + oIO;
     b.rgba = g + org;
-    b.dists = bt.dists;
+    b.dists = dists;
     b.alpha = g + oal;
     b.cp = g + ocp;
     b.wsamp = g + ows;
@@ -761,7 +771,7 @@ extern "C" int lnerf_train_step(lnerf_ctx* ctx, const lnerf_mlp* mlp, const floa
         if (!(flags & LNERF_WANT_DX)) o.d_x = nullptr;
         std::lock_guard<std::mutex> lock(ctx->mu);
         HIP_OK(hipSetDevice(ctx->device));
-        hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+        hipStream_t s = (hipStream_t)stream;   // NULL: the device's default (null) stream
         if (use_fused(*mlp, *batch, flags)) {
             const size_t bytes = fused_workspace_bytes(*mlp, batch->rays, batch->samples);
             FusedPlan p{};
@@ -777,6 +787,15 @@ extern "C" int lnerf_train_step(lnerf_ctx* ctx, const lnerf_mlp* mlp, const floa
     });
 }
 
+extern "C" int lnerf_get_rays(int width, const double* K, const double* c2w, float* rays,
+                              void* stream) {
+    return guard_int([&]() {
+        if (width < 1 || !K || !c2w || !rays) fail("lnerf_get_rays: bad arguments");
+        k_get_rays(width, K, c2w, rays, (hipStream_t)stream);
+        check_launch("lnerf_get_rays");
+    });
+}
+
 extern "C" int lnerf_render(lnerf_ctx* ctx, const lnerf_mlp* mlp, const float* ws, const float* bs,
                             const lnerf_batch* batch, const lnerf_outputs* out, void* stream) {
     return guard_int([&]() {
@@ -785,7 +804,7 @@ extern "C" int lnerf_render(lnerf_ctx* ctx, const lnerf_mlp* mlp, const float* w
         lnerf_outputs o = out ? *out : lnerf_outputs{};
         std::lock_guard<std::mutex> lock(ctx->mu);
         HIP_OK(hipSetDevice(ctx->device));
-        hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+        hipStream_t s = (hipStream_t)stream;   // NULL: the device's default (null) stream
         if (use_fused(*mlp, *batch, 0)) {
             const size_t bytes = fused_workspace_bytes(*mlp, batch->rays, batch->samples);
             FusedPlan p{};

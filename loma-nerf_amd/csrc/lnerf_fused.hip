@@ -56,6 +56,7 @@ struct FusedArgs {
     float* grad;
     size_t grad_off[kMaxLayers];
     int rays, S, rpw, R, input_mode, F;
+    float near_t, far_t;          // RAYS mode sampling range
     const float* x;
     const float* dists;
     const float* target;
@@ -393,15 +394,24 @@ __device__ __forceinline__ void layer_mma_n(const FusedArgs& a, bool fwd, int l,
     else layer_mma<8, X6>(a, fwd, l, nchunks, in, out, ring, tstore, tr, nullptr, nullptr);
 }
 
+// Coordinate c of sample row gs: the given point (POINTS) or o + d t in float64 (RAYS).
+__device__ __forceinline__ double sample_coord(const FusedArgs& a, int gs, int c) {
+    if (a.input_mode == LNERF_INPUT_RAYS) {
+        const int ray = gs / a.S, j = gs - ray * a.S;
+        return ray_point(a.x + (size_t)ray * 6, c, j, a.S, a.near_t, a.far_t);
+    }
+    return (double)a.x[(size_t)gs * 3 + c];
+}
+
 __device__ __forceinline__ float input_feature(const FusedArgs& a, int gs, bool valid, int f) {
     if (!valid || f >= a.k0) return 0.0f;
     if (a.input_mode == LNERF_INPUT_ENCODED) return a.x[(size_t)gs * a.k0 + f];
     // positional_encoding_3d (pos_encoding.py:54-66): block-major, float64 trig, rounded once
     const int c = f % 3, blk = f / 3;
-    const float xc = a.x[(size_t)gs * 3 + c];
-    if (blk == 0) return xc;
+    const double xc = sample_coord(a, gs, c);
+    if (blk == 0) return (float)xc;
     const int fb = blk - 1, freq = fb >> 1;
-    const double arg = ldexp((double)xc, freq);
+    const double arg = ldexp(xc, freq);
     return (fb & 1) ? (float)cos(arg) : (float)sin(arg);
 }
 
@@ -462,7 +472,7 @@ __device__ __forceinline__ float composite_tile(const FusedArgs& a, int wg, floa
 #pragma unroll
         for (int k = 0; k < 3; ++k) rgb[k] = 1.0f / (1.0f + expf(0.0f - z[k]));
         sigma = (z[3] > 0.0f) ? z[3] : 0.0f;
-        delta = a.dists[gs];
+        delta = a.dists ? a.dists[gs] : ray_delta(j, S, a.near_t, a.far_t);
         al = 1.0f - expf((0.0f - sigma) * delta);
         cc = (1.0f - al) + (float)(1e-10);
     }
@@ -600,19 +610,19 @@ __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs 
     for (int t = 0; t < kNT; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) act[t][r] = 0.0f;
-    if (a.input_mode == LNERF_INPUT_POINTS && a.k0 <= 64) {
+    if (a.input_mode != LNERF_INPUT_ENCODED && a.k0 <= 64) {
         constexpr int kStride = 65;
         float* pe = ldsw + (size_t)wave * (32 * kStride);
         const int F = a.F, per = 3 * (F + 1);
         for (int it = lane; it < 32 * per; it += 64) {
             const int sl = it / per, rem = it - sl * per, c = rem % 3, q = rem / 3;
             const bool vs = (wave * 32 + sl < tile_samples) && (tile_base + sl < a.R);
-            const float xc = vs ? a.x[(size_t)(tile_base + sl) * 3 + c] : 0.0f;
+            const double xc = vs ? sample_coord(a, tile_base + sl, c) : 0.0;
             if (q == 0) {
-                pe[sl * kStride + c] = xc;
+                pe[sl * kStride + c] = (float)xc;
             } else {
                 double sn, cs;
-                sincos(ldexp((double)xc, q - 1), &sn, &cs);
+                sincos(ldexp(xc, q - 1), &sn, &cs);
                 pe[sl * kStride + 3 + 6 * (q - 1) + c] = (float)sn;
                 pe[sl * kStride + 6 + 6 * (q - 1) + c] = (float)cs;
             }
@@ -1430,8 +1440,10 @@ static FusedArgs make_fused_args(const FusedPlan& p, const lnerf_batch& b, float
     a.R = p.R;
     a.input_mode = b.input_mode;
     a.F = b.num_freqs;
+    a.near_t = b.near_t;
+    a.far_t = b.far_t;
     a.x = b.x;
-    a.dists = b.dists;
+    a.dists = b.input_mode == LNERF_INPUT_RAYS ? nullptr : b.dists;
     a.target = b.target;
     a.loss_part = p.loss_part;
     a.acc_color = out.acc_color;

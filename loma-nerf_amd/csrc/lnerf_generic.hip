@@ -351,6 +351,50 @@ __global__ void pe_kernel(const float* __restrict__ pts, int n, int F, float* ou
             o[3 + 6 * f + 3 + c] = (float)cos(x);
         }
 }
+// RAYS mode: sample points o + d t in float64 (train_nerf.py:295-299), encoded like pe_kernel.
+__global__ void pe_rays_kernel(const float* __restrict__ rays, int nrays, int S, float near_t,
+                               float far_t, int F, float* out, int out_cols) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nrays * S) return;
+    const int ray = s / S, j = s - ray * S;
+    float* o = out + (size_t)s * out_cols;
+    for (int c = 0; c < 3; ++c) {
+        const double p = ray_point(rays + (size_t)ray * 6, c, j, S, near_t, far_t);
+        o[c] = (float)p;
+        for (int f = 0; f < F; ++f) {
+            const double x = ldexp(p, f);
+            o[3 + 6 * f + c] = (float)sin(x);
+            o[3 + 6 * f + 3 + c] = (float)cos(x);
+        }
+    }
+}
+__global__ void ray_dists_kernel(int n, int S, float near_t, float far_t, float* out) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < n) out[s] = ray_delta(s % S, S, near_t, far_t);
+}
+// get_rays, train_nerf.py:23-62 (float64 math, float32 [o, d] rows)
+struct RayCam {
+    double K[9];
+    double c2w[12];
+};
+__global__ void get_rays_kernel(int width, RayCam cam, float* rays) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= width * width) return;
+    const int row = p / width, col = p - row * width;
+    // np.linspace(0, 1, width): k * step, the last exactly 1
+    const double step = width > 1 ? 1.0 / (double)(width - 1) : 0.0;
+    const double i = (col == width - 1 && width > 1) ? 1.0 : (double)col * step;
+    const double j = (row == width - 1 && width > 1) ? 1.0 : (double)row * step;
+    const double dir[3] = {(i - cam.K[2]) / cam.K[0], -(j - cam.K[5]) / cam.K[4], -1.0};
+    float* r = rays + (size_t)p * 6;
+    for (int a = 0; a < 3; ++a) {
+        r[a] = (float)cam.c2w[a * 4 + 3];
+        double d = 0.0;
+        for (int b = 0; b < 3; ++b) d += dir[b] * cam.c2w[a * 4 + b];   // directions @ R.T
+        r[3 + a] = (float)d;
+    }
+}
+
 // Adam, train_nerf.py:143-161 (lr_t folds sqrt(1-b2^t)/(1-b1^t); m_hat/v_hat as written there).
 __global__ void adam_kernel(float* p, const float* __restrict__ g, float* m, float* v, size_t n,
                             float lr_t, float b1, float b2, float eps, float bc1, float bc2) {
@@ -450,6 +494,22 @@ void k_scale_by_scalar(float* p, size_t n, const float* scale, hipStream_t s) {
 void k_positional_encoding(const float* pts, int n, int F, float* out, int out_cols,
                            hipStream_t s) {
     if (n > 0) pe_kernel<<<(n + 255) / 256, 256, 0, s>>>(pts, n, F, out, out_cols);
+}
+void k_positional_encoding_rays(const float* rays, int nrays, int S, float near_t, float far_t,
+                                int F, float* out, int out_cols, hipStream_t s) {
+    const int n = nrays * S;
+    if (n > 0) pe_rays_kernel<<<(n + 255) / 256, 256, 0, s>>>(rays, nrays, S, near_t, far_t, F, out, out_cols);
+}
+void k_ray_dists(int nrays, int S, float near_t, float far_t, float* out, hipStream_t s) {
+    const int n = nrays * S;
+    if (n > 0) ray_dists_kernel<<<(n + 255) / 256, 256, 0, s>>>(n, S, near_t, far_t, out);
+}
+void k_get_rays(int width, const double* K, const double* c2w, float* rays, hipStream_t s) {
+    RayCam cam;
+    for (int i = 0; i < 9; ++i) cam.K[i] = K[i];
+    for (int i = 0; i < 12; ++i) cam.c2w[i] = c2w[i];
+    const int n = width * width;
+    if (n > 0) get_rays_kernel<<<(n + 255) / 256, 256, 0, s>>>(width, cam, rays);
 }
 void k_adam(float* params, const float* grads, float* m, float* v, size_t n, int t, float lr,
             float beta1, float beta2, float eps, hipStream_t s) {

@@ -11,6 +11,24 @@ namespace lnerf {
 
 constexpr int kMaxLayers = LNERF_MAX_LAYERS;
 
+// ---- ray sampling (train_nerf.py:289-306), float64 as numpy computes it -----------------------
+// t_j = np.linspace(near, far, S)[j]: j * ((far - near) / (S - 1)) + near, the last one = far.
+__host__ __device__ inline double ray_depth(int j, int S, float near_t, float far_t) {
+    if (S <= 1) return (double)near_t;
+    if (j == S - 1) return (double)far_t;
+    return (double)j * (((double)far_t - (double)near_t) / (double)(S - 1)) + (double)near_t;
+}
+// dists_j = t_{j+1} - t_j, the last 1e8 (then float32 at the ABI)
+__host__ __device__ inline float ray_delta(int j, int S, float near_t, float far_t) {
+    if (j >= S - 1) return 1e8f;
+    return (float)(ray_depth(j + 1, S, near_t, far_t) - ray_depth(j, S, near_t, far_t));
+}
+// coordinate c of sample j of a ray [o, d]: o + d * t (pts = o + d * t[None, :, None])
+__host__ __device__ inline double ray_point(const float* ray6, int c, int j, int S, float near_t,
+                                            float far_t) {
+    return (double)ray6[c] + (double)ray6[3 + c] * ray_depth(j, S, near_t, far_t);
+}
+
 // ----------------------------------------------------------------------------------------------
 // Generic ("loma-order") path: one loma call on flat device rectangles. Field meaning follows
 // scripts/nerf.py:1-22; loop bounds are exactly the reference's.
@@ -79,6 +97,12 @@ void lg_mult_a_b(const float* a, int a_h, int a_w, const float* b, int b_w, floa
 // small helpers
 void k_fill(float* p, float v, size_t n, hipStream_t s);
 void k_scale_by_scalar(float* p, size_t n, const float* scale, hipStream_t s);
+// RAYS mode producers for the generic path: the encoded sample rows (f64 points, f64 trig) and
+// the per-sample dists.
+void k_positional_encoding_rays(const float* rays, int nrays, int S, float near_t, float far_t,
+                                int F, float* out, int out_cols, hipStream_t s);
+void k_ray_dists(int nrays, int S, float near_t, float far_t, float* out, hipStream_t s);
+void k_get_rays(int width, const double* K, const double* c2w, float* rays, hipStream_t s);
 void k_positional_encoding(const float* pts, int n, int F, float* out, int out_cols,
                            hipStream_t s);
 void k_adam(float* params, const float* grads, float* m, float* v, size_t n, int t, float lr,

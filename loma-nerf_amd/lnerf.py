@@ -19,6 +19,7 @@ MAX_LAYERS = 16
 
 INPUT_ENCODED = 0
 INPUT_POINTS = 1
+INPUT_RAYS = 2
 SEED_CONST = 0
 SEED_LOSS = 1
 ACCUMULATE = 2
@@ -33,7 +34,7 @@ EXPORTED_SYMBOLS = [
     "nerf_evaluate_and_march", "grad_nerf_evaluate_and_march", "mlp_fit", "grad_mlp_fit",
     "mult_a_b", "lnerf_last_error", "lnerf_version", "lnerf_ctx_create", "lnerf_ctx_destroy",
     "lnerf_workspace_bytes", "lnerf_train_step", "lnerf_render", "lnerf_scale_by_device_scalar",
-    "lnerf_adam_update", "lnerf_ctx_timings",
+    "lnerf_adam_update", "lnerf_ctx_timings", "lnerf_get_rays",
 ]
 
 
@@ -45,7 +46,7 @@ class LnerfMLP(ctypes.Structure):
 class LnerfBatch(ctypes.Structure):
     _fields_ = [("rays", ctypes.c_int), ("samples", ctypes.c_int), ("input_mode", ctypes.c_int),
                 ("num_freqs", ctypes.c_int), ("x", ctypes.c_void_p), ("dists", ctypes.c_void_p),
-                ("target", ctypes.c_void_p)]
+                ("target", ctypes.c_void_p), ("near_t", ctypes.c_float), ("far_t", ctypes.c_float)]
 
 
 class LnerfOutputs(ctypes.Structure):
@@ -137,8 +138,10 @@ def configure(lib: ctypes.CDLL) -> None:
                                       ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_float,
                                       ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
     lib.lnerf_ctx_timings.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
+    lib.lnerf_get_rays.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                   ctypes.POINTER(ctypes.c_double), ctypes.c_void_p, ctypes.c_void_p]
     for name in ("lnerf_ctx_timings", "lnerf_ctx_create", "lnerf_train_step", "lnerf_render",
-                 "lnerf_scale_by_device_scalar", "lnerf_adam_update"):
+                 "lnerf_scale_by_device_scalar", "lnerf_adam_update", "lnerf_get_rays"):
         getattr(lib, name).restype = ctypes.c_int
 
 
@@ -203,16 +206,22 @@ class Engine:
         g = self.torch.zeros(nW + nB + 1, dtype=self.torch.float32, device=f"cuda:{self.device}")
         return g, g[:nW].view(L, w_k, w_n), g[nW:nW + nB].view(L, w_n), g[nW + nB:]
 
+    @staticmethod
+    def _batch(rays, samples, input_mode, num_freqs, x, dists, target, near, far):
+        return LnerfBatch(rays, samples, input_mode, num_freqs, x.data_ptr(),
+                          None if dists is None else dists.data_ptr(), target.data_ptr(),
+                          float(near), float(far))
+
     def train_step(self, mlp: LnerfMLP, ws, bs, x, dists, target, *, samples: int,
                    input_mode: int = INPUT_POINTS, num_freqs: int = 5, seed=None, flags: int = 0,
                    grads=None, want_per_ray: bool = False, want_dx: bool = False,
-                   acc_color=None) -> StepResult:
+                   acc_color=None, near: float = 2.0, far: float = 6.0) -> StepResult:
         """One fwd+bwd over the batch. seed=None seeds with the batch loss (train_nerf.py:477);
-        a float seeds with that constant. `grads` (from alloc_grads) is reused if given."""
+        a float seeds with that constant. `grads` (from alloc_grads) is reused if given.
+        INPUT_RAYS: x = (rays, 6) [o, d], dists=None, samples at linspace(near, far, S)."""
         torch = self.torch
         rays = target.shape[0]
-        b = LnerfBatch(rays, samples, input_mode, num_freqs, x.data_ptr(), dists.data_ptr(),
-                       target.data_ptr())
+        b = self._batch(rays, samples, input_mode, num_freqs, x, dists, target, near, far)
         if grads is None:
             grads = self.alloc_grads(mlp.num_layers, mlp.w_k, mlp.w_n)
         g, dws, dbs, loss = grads
@@ -240,11 +249,11 @@ class Engine:
         return StepResult(loss[0], acc_color, g, dws, dbs, d_dists, d_target, d_x)
 
     def render(self, mlp: LnerfMLP, ws, bs, x, dists, target, *, samples: int,
-               input_mode: int = INPUT_POINTS, num_freqs: int = 5):
+               input_mode: int = INPUT_POINTS, num_freqs: int = 5, near: float = 2.0,
+               far: float = 6.0):
         torch = self.torch
         rays = target.shape[0]
-        b = LnerfBatch(rays, samples, input_mode, num_freqs, x.data_ptr(), dists.data_ptr(),
-                       target.data_ptr())
+        b = self._batch(rays, samples, input_mode, num_freqs, x, dists, target, near, far)
         acc = torch.empty(rays, 3, dtype=torch.float32, device=target.device)
         loss = torch.empty(1, dtype=torch.float32, device=target.device)
         o = LnerfOutputs(loss.data_ptr(), acc.data_ptr(), None, None, None, None, None)
@@ -253,6 +262,20 @@ class Engine:
         if rc != 0:
             raise RuntimeError(f"lnerf_render: {last_error()}")
         return loss[0], acc
+
+    def get_rays(self, width: int, K, c2w):
+        """train_nerf.py:23-62 on the device: (width*width, 6) float32 rays [o, d]."""
+        import numpy as np
+        torch = self.torch
+        Kd = np.ascontiguousarray(np.asarray(K, np.float64).reshape(3, 3))
+        cd = np.ascontiguousarray(np.asarray(c2w, np.float64)[:3, :4])
+        out = torch.empty(width * width, 6, dtype=torch.float32, device=f"cuda:{self.device}")
+        dp = ctypes.POINTER(ctypes.c_double)
+        rc = self.lib.lnerf_get_rays(width, Kd.ctypes.data_as(dp), cd.ctypes.data_as(dp),
+                                     ctypes.c_void_p(out.data_ptr()), self._stream())
+        if rc != 0:
+            raise RuntimeError(f"lnerf_get_rays: {last_error()}")
+        return out
 
     def timings(self):
         """Per-kernel ms of the last TIMING step: pack, fused, loss, dw, reduce, total."""

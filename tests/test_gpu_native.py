@@ -264,3 +264,79 @@ def test_adam_matches_reference_update(engine):
         engine.adam_update(pd, gd, md, vd, t, lr, b1, b2, eps)
     torch.cuda.synchronize()
     assert np.allclose(pd.cpu().numpy(), p, rtol=1e-5, atol=1e-7)
+
+
+# ---- on-device producers: get_rays and RAYS input mode ------------------------
+
+def _rays_reference(w_rays32, S, F, near=2.0, far=6.0):
+    """numpy restatement of the RAYS producers (train_nerf.py:289-306) from the float32 rays the
+    device consumes: f64 points o + d t, f64 PE rounded once, dists [diff(t), 1e8]."""
+    o = w_rays32[:, :3].astype(np.float64)
+    d = w_rays32[:, 3:].astype(np.float64)
+    pts, dists = nerf_np.sample_rays(o, d, S, near, far)
+    X = nerf_np.positional_encoding_3d(pts, F).reshape(-1, 3 + 6 * F)
+    return X, dists.astype(np.float32)
+
+
+@pytest.mark.parametrize("generic", [False, True])
+def test_rays_mode_matches_oracle(engine, generic):
+    import lnerf
+    import oracle
+    import torch
+    w = nerf_np.make_workload("cfg2", rays=96, samples=32)
+    focal = 0.5 / np.tan(0.5 * 0.6911112)
+    K = np.array([[focal, 0, 0.5], [0, focal, 0.5], [0, 0, 1]], np.float32)
+    o, d = nerf_np.get_rays(100, 100, K, nerf_np.look_at_pose())
+    sel = np.random.RandomState(5).choice(o.shape[0], 96, replace=False)
+    rays32 = np.concatenate([o[sel], d[sel]], 1).astype(np.float32)
+    X, dists = _rays_reference(rays32, w.S, w.F)
+    shapes = [x.shape for x in w.ws]
+    want = oracle.standard_forward_backward(X, w.wp, w.bp, shapes, dists, w.target, w.S, seed=None)
+    mlp = lnerf.make_mlp(shapes, w.wp.shape[1], w.wp.shape[2])
+    r = engine.train_step(mlp, _dev(engine, w.wp), _dev(engine, w.bp), _dev(engine, rays32), None,
+                          _dev(engine, w.target), samples=w.S, input_mode=lnerf.INPUT_RAYS,
+                          num_freqs=w.F, want_per_ray=True,
+                          flags=lnerf.GENERIC if generic else lnerf.FAST)
+    torch.cuda.synchronize()
+    got = dict(loss=float(r.loss.item()), acc=r.acc_color.cpu().numpy(), dW=r.d_ws.cpu().numpy(),
+               dB=r.d_bs.cpu().numpy(), d_dists=r.d_dists.cpu().numpy(),
+               d_target=r.d_target.cpu().numpy())
+    compare(got, want)
+
+
+def test_get_rays_matches_reference_restatement(engine):
+    import torch
+    focal = 0.5 / np.tan(0.5 * 0.6911112)
+    K = np.array([[focal, 0, 0.5], [0, focal, 0.5], [0, 0, 1]], np.float32)
+    c2w = nerf_np.look_at_pose(azimuth_deg=-30.0, elevation_deg=20.0)
+    for width in (1, 2, 37, 400):
+        got = engine.get_rays(width, K.astype(np.float64), c2w)
+        torch.cuda.synchronize()
+        o, d = nerf_np.get_rays(width, width, K, c2w)
+        want = np.concatenate([o, d], 1).astype(np.float32)
+        np.testing.assert_allclose(got.cpu().numpy(), want, rtol=1e-6, atol=1e-6)
+
+
+def test_rays_mode_full_size_equals_points_mode(engine, full):
+    """cfg3 at full size: RAYS mode (device sampling) vs POINTS mode fed the device's own points
+    path on the same rays -- same loss and gradients within the fp32 tolerance."""
+    import lnerf
+    import torch
+    focal = 0.5 / np.tan(0.5 * 0.6911112)
+    K = np.array([[focal, 0, 0.5], [0, focal, 0.5], [0, 0, 1]], np.float32)
+    rays_all = engine.get_rays(400, K.astype(np.float64), nerf_np.look_at_pose())
+    sel = torch.from_numpy(np.random.RandomState(0).choice(400 * 400, 4096, replace=False)).to(rays_all.device)
+    rays = rays_all.index_select(0, sel).contiguous()
+    X, dists = _rays_reference(rays.cpu().numpy(), 64, 5)
+    shapes = [x.shape for x in full.ws]
+    mlp = lnerf.make_mlp(shapes, full.wp.shape[1], full.wp.shape[2])
+    ws, bs, tgt = _dev(engine, full.wp), _dev(engine, full.bp), _dev(engine, full.target)
+    a = engine.train_step(mlp, ws, bs, rays, None, tgt, samples=64, input_mode=lnerf.INPUT_RAYS,
+                          num_freqs=5, seed=1.0, flags=lnerf.FAST)
+    ga = (float(a.loss.item()), a.d_ws.cpu().numpy().copy(), a.acc_color.cpu().numpy().copy())
+    b = engine.train_step(mlp, ws, bs, _dev(engine, X), _dev(engine, dists), tgt, samples=64,
+                          input_mode=lnerf.INPUT_ENCODED, seed=1.0, flags=lnerf.FAST)
+    torch.cuda.synchronize()
+    assert abs(ga[0] - float(b.loss.item())) <= 1e-5 * abs(ga[0])
+    assert_close("acc", ga[2], b.acc_color.cpu().numpy(), **TOL)
+    assert_close("dW", ga[1], b.d_ws.cpu().numpy(), **TOL)

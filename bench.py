@@ -3,10 +3,11 @@
 
 Workload (BASELINE.json configs[2]): synthetic Lego-style 400x400 camera,
 4096 rays x 64 samples per GPU, positional encoding F=5 (33 inputs), MLP 33->256x7->4, fp32,
-random-init weights (mlp_utils.py:166-204, seed 215). A step = positional encoding + MLP forward
-+ compositing + sum-of-squares loss + the reverse pass over every MLP weight (the work of one
-nerf_evaluate_and_march + grad_nerf_evaluate_and_march pair on the batch), on inputs already
-resident in HBM. With N > 1 GPUs (one process per GPU, torchrun) every rank runs its own 4096-ray
+random-init weights (mlp_utils.py:166-204, seed 215). A step = sampling the rays (linspace depths,
+points, dists; train_nerf.py:289-306) + positional encoding + MLP forward + compositing +
+sum-of-squares loss + the reverse pass over every MLP weight (the work of one
+nerf_evaluate_and_march + grad_nerf_evaluate_and_march pair on the batch), on rays already
+resident in HBM (--input points: host-sampled points instead). With N > 1 GPUs (one process per GPU, torchrun) every rank runs its own 4096-ray
 batch (weak scaling) and the packed [dW, db, loss] buffer is all-reduced (SUM) over RCCL, then
 scaled by the global loss (the reference seeds its gradient with the loss, train_nerf.py:477).
 
@@ -43,6 +44,9 @@ def parse():
     ap.add_argument("--cpu-rays", type=int, default=128, help="rays in the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--generic", action="store_true", help="time the loma-order kernels instead")
+    ap.add_argument("--input", choices=("rays", "points"), default="rays",
+                    help="rays: (rays, 6) origins+directions, the engine samples points, dists and "
+                         "the encoding on the GPU (LNERF_INPUT_RAYS); points: host-sampled positions")
     ap.add_argument("--mfma-f32", action="store_true",
                     help="fused path with exact f32 MFMA products instead of the bf16x6 split")
     return ap.parse_args()
@@ -120,8 +124,14 @@ def main():
     mlp = lnerf.make_mlp(shapes, wp.shape[1], wp.shape[2])
     ws = torch.from_numpy(wp).to(dev)
     bs = torch.from_numpy(bp).to(dev)
-    pts = torch.from_numpy(b["pts"]).to(dev)
-    dists = torch.from_numpy(b["dists"]).to(dev)
+    if args.input == "rays":
+        x = torch.from_numpy(b["rays"]).to(dev)
+        dists = None
+        mode = lnerf.INPUT_RAYS
+    else:
+        x = torch.from_numpy(b["pts"]).to(dev)
+        dists = torch.from_numpy(b["dists"]).to(dev)
+        mode = lnerf.INPUT_POINTS
     target = torch.from_numpy(b["target"]).to(dev)
     grads = eng.alloc_grads(len(shapes), wp.shape[1], wp.shape[2])
     gbuf = grads[0]
@@ -133,10 +143,10 @@ def main():
     def step(timing=False):
         f = flags | (lnerf.TIMING if timing else 0)
         if dist is None:
-            eng.train_step(mlp, ws, bs, pts, dists, target, samples=S, num_freqs=b["F"],
+            eng.train_step(mlp, ws, bs, x, dists, target, samples=S, num_freqs=b["F"], input_mode=mode,
                            seed=None, flags=f, grads=grads, acc_color=acc)
         else:
-            eng.train_step(mlp, ws, bs, pts, dists, target, samples=S, num_freqs=b["F"],
+            eng.train_step(mlp, ws, bs, x, dists, target, samples=S, num_freqs=b["F"], input_mode=mode,
                            seed=1.0, flags=f, grads=grads, acc_color=acc)
             # [dW, db, loss] SUM over ranks (RCCL), then the loss seed (loma-nerf_amd/dp.py)
             dp.allreduce_loss_seeded(gbuf, dist, eng.scale_by_device_scalar)
@@ -187,7 +197,9 @@ def main():
             "config": {"workload": f"{args.config}: {N} rays x {S} samples per GPU, PE F={b['F']}, "
                                    f"MLP {shapes[0][0]}->{b['H']}x{b['L'] - 1}->4, fp32",
                        "rays_per_gpu": N, "samples": S, "layers": b["L"], "width": b["H"],
-                       "parallelism": f"dp{world}", "path": "generic" if args.generic else "fused"},
+                       "parallelism": f"dp{world}", "path": "generic" if args.generic else "fused",
+                       "input": ("rays: sampling, dists and positional encoding on the GPU"
+                                 if args.input == "rays" else "points: sampled on the host")},
             "step_tflops": step_flops / (ms / 1e3) / 1e12,
         }
         if kt:

@@ -77,8 +77,9 @@ def make_batch(name="cfg3", rays=None, samples=None, rank=0):
     pts = o[sel][:, None, :] + d[sel][:, None, :] * t[None, :, None]
     dists = np.concatenate((t[1:] - t[:-1], [1e8]))[None, :].repeat(N, 0)
     target = np.random.RandomState(1 + 1000 * rank).uniform(0, 1, size=(N, 3)).astype(np.float32)
+    rays = np.concatenate([o[sel], d[sel]], 1).astype(np.float32)   # LNERF_INPUT_RAYS rows
     return dict(pts=pts.reshape(-1, 3).astype(np.float32), dists=dists.astype(np.float32),
-                target=target, F=F, S=S, N=N, L=L, H=H)
+                rays=rays, target=target, F=F, S=S, N=N, L=L, H=H)
 
 
 def step_flops(shapes):

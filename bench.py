@@ -47,6 +47,10 @@ def parse():
     ap.add_argument("--input", choices=("rays", "points"), default="rays",
                     help="rays: (rays, 6) origins+directions, the engine samples points, dists and "
                          "the encoding on the GPU (LNERF_INPUT_RAYS); points: host-sampled positions")
+    ap.add_argument("--render", action="store_true",
+                    help="config 5 instead: forward-only eval render of an 800x800 frame at 128 "
+                         "samples/ray (bf16 MFMA unless --x6/--mfma-f32), rays sharded over ranks")
+    ap.add_argument("--x6", action="store_true", help="render with the fp32-accurate bf16x6 path")
     ap.add_argument("--mfma-f32", action="store_true",
                     help="fused path with exact f32 MFMA products instead of the bf16x6 split")
     return ap.parse_args()
@@ -98,6 +102,81 @@ def cpu_baseline(args, cfg):
              "sample": f"{rn} rays x {b['S']} samples, OpenMP over rays, {tn:.1f}s"})
 
 
+def bench_render(args, world, rank, local, dist):
+    """Config 5: 800x800 frame, 128 samples/ray, MLP 33->256x7->4, forward only.
+    The frame's 640 000 rays come from the device get_rays; each rank renders a contiguous share
+    (replicas, no collective in the timed region)."""
+    import numpy as np
+    import torch
+    import dp
+    import lnerf
+    import scene
+    side, _, S, F, L, H = scene.CONFIGS["cfg5"]
+    dev = f"cuda:{local}"
+    eng = lnerf.Engine(local)
+    shapes, wp, bp = scene.init_mlp(3 + 6 * F, 4, L, H)
+    mlp = lnerf.make_mlp(shapes, wp.shape[1], wp.shape[2])
+    ws = torch.from_numpy(wp).to(dev)
+    bs = torch.from_numpy(bp).to(dev)
+    focal = 0.5 / np.tan(0.5 * scene.CAMERA_ANGLE_X)
+    K = np.array([[focal, 0, 0.5], [0, focal, 0.5], [0, 0, 1]])
+    rays_all = eng.get_rays(side, K, scene.look_at_pose())
+    lo, hi = dp.shard_rays(rays_all.shape[0], world, rank)
+    rays = rays_all[lo:hi].contiguous()
+    N = rays.shape[0]
+    target = torch.zeros(N, 3, dtype=torch.float32, device=dev)
+    acc = torch.empty(N, 3, dtype=torch.float32, device=dev)
+    loss = torch.empty(1, dtype=torch.float32, device=dev)
+    flags = lnerf.FAST | (lnerf.MFMA_F32 if args.mfma_f32 else 0 if args.x6 else lnerf.MFMA_BF16)
+
+    def step():
+        eng.render(mlp, ws, bs, rays, None, target, samples=S, input_mode=lnerf.INPUT_RAYS,
+                   num_freqs=F, flags=flags, acc=acc, loss=loss)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms = dt / args.steps * 1e3
+    total = side * side * S
+    fwd_flops = 2 * sum(k * n for k, n in shapes)
+    if rank == 0:
+        mode = "f32" if args.mfma_f32 else "bf16x6" if args.x6 else "bf16"
+        peak = PEAK_FP32_TFLOPS if args.mfma_f32 else PEAK_X6_TFLOPS if args.x6 else PEAK_BF16_TFLOPS
+        ach = fwd_flops * N * S / (ms / 1e3) / 1e12
+        print(json.dumps({
+            "metric": "ray-samples/sec fwd (eval render), 800x800 frame x 128 samples",
+            "value": total / (ms / 1e3), "unit": "ray-samples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": mode, "data": "synthetic (device get_rays of a look-at camera, random-init "
+                                   "MLP seed 215)",
+            "config": {"workload": "cfg5: 800x800 rays x 128 samples per frame, PE F=5, "
+                                   "MLP 33->256x7->4, forward only",
+                       "rays_per_gpu": N, "parallelism": f"replicas{world}"},
+            "roofline": {"bound": "mfma", "kernel": "fused_fwd_bwd_kernel (forward only)",
+                         "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,
+                         "traffic": None,
+                         "note": "rank-0 per-GPU rate: 2*sum(KN) FLOP/sample x its samples / "
+                                 "step time (includes get_rays-free sampling + PE + compositing)"},
+        }), flush=True)
+    eng.close()
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -116,6 +195,11 @@ def main():
     if world > 1 or "WORLD_SIZE" in os.environ:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    if args.render:
+        bench_render(args, world, rank, local, dist)
+        if dist:
+            dist.destroy_process_group()
+        return
     dev = f"cuda:{local}"
     b = scene.make_batch(args.config, rays=args.rays, rank=rank)
     shapes, wp, bp = scene.init_mlp(3 + 6 * b["F"], 4, b["L"], b["H"])

@@ -130,9 +130,11 @@ enum {
     LNERF_GENERIC = 8,        /* force the stage-by-stage loma-order kernels (no MFMA fusion) */
     LNERF_FAST = 16,          /* require the fused MFMA path (error if the shape is unsupported) */
     LNERF_TIMING = 32,        /* record per-kernel HIP events (read with lnerf_ctx_timings)   */
-    LNERF_MFMA_F32 = 64       /* fused path: exact f32 MFMA products instead of the default
+    LNERF_MFMA_F32 = 64,      /* fused path: exact f32 MFMA products instead of the default
                                  bf16x6 split (x = hi+mid+lo in bf16, six bf16 MFMAs per
                                  product, fp32-accurate: dropped terms <= 2^-24 |w x|)         */
+    LNERF_MFMA_BF16 = 128     /* fused path: plain bf16 operands, fp32 accumulate (one MFMA per
+                                 product; reduced precision -- inference / config 5 render)   */
 };
 
 /* Optional outputs (device pointers; any may be NULL). */
@@ -169,7 +171,7 @@ int lnerf_get_rays(int width, const double* K, const double* c2w, float* rays, v
 
 /* Forward only (eval render, train_nerf.py:616-661): acc_color and, if target != NULL, loss. */
 int lnerf_render(lnerf_ctx* ctx, const lnerf_mlp* mlp, const float* ws, const float* bs,
-                 const lnerf_batch* batch, const lnerf_outputs* out, void* stream);
+                 const lnerf_batch* batch, int flags, const lnerf_outputs* out, void* stream);
 
 /* Per-kernel times (ms) of the last LNERF_TIMING step on `ctx`, measured with HIP events on the
  * step's stream: [0] weight pack, [1] fused fwd+reverse-chain kernel, [2] loss reduce,

@@ -797,7 +797,8 @@ extern "C" int lnerf_get_rays(int width, const double* K, const double* c2w, flo
 }
 
 extern "C" int lnerf_render(lnerf_ctx* ctx, const lnerf_mlp* mlp, const float* ws, const float* bs,
-                            const lnerf_batch* batch, const lnerf_outputs* out, void* stream) {
+                            const lnerf_batch* batch, int flags, const lnerf_outputs* out,
+                            void* stream) {
     return guard_int([&]() {
         if (!ctx) fail("null ctx");
         validate(mlp, batch);
@@ -805,10 +806,10 @@ extern "C" int lnerf_render(lnerf_ctx* ctx, const lnerf_mlp* mlp, const float* w
         std::lock_guard<std::mutex> lock(ctx->mu);
         HIP_OK(hipSetDevice(ctx->device));
         hipStream_t s = (hipStream_t)stream;   // NULL: the device's default (null) stream
-        if (use_fused(*mlp, *batch, 0)) {
-            const size_t bytes = fused_workspace_bytes(*mlp, batch->rays, batch->samples);
+        if (use_fused(*mlp, *batch, flags & ~LNERF_WANT_DX)) {
+            const size_t bytes = fused_workspace_bytes(*mlp, batch->rays, batch->samples, false);
             FusedPlan p{};
-            fused_plan(p, *mlp, *batch, ctx->fused_ws.get(bytes), 0);
+            fused_plan(p, *mlp, *batch, ctx->fused_ws.get(bytes), flags, false);
             fused_render(p, ws, bs, *batch, o, s);
         } else {
             generic_step(ctx, *mlp, ws, bs, *batch, 1.0f, 0, o, false, s);

@@ -195,7 +195,7 @@ __device__ __forceinline__ void mma_stream_t(const float* __restrict__ src, int 
 }
 
 // Output-tile counts are rounded up to 1/2/4/8 (the padded tiles of the packed weights are zero).
-template <bool X6>
+template <int PREC>
 __device__ __forceinline__ void layer_mma_n(const FusedArgs& a, bool fwd, int l, int nchunks, int nto,
                                             const fx16 (&in)[kNT], fx16 (&out)[kNT],
                                             unsigned char* ring, float* tstore, float* tr);
@@ -251,24 +251,38 @@ __device__ __forceinline__ bf8 ds_read_b128_at(unsigned addr) {
     return r;
 }
 
-// s_waitcnt lgkmcnt(N) that the three fragments depend on (so no use can be scheduled above it).
+// s_waitcnt lgkmcnt(N) that the fragments depend on (so no use can be scheduled above it).
 template <int N>
 __device__ __forceinline__ void lgkm_wait_for(bf8& a, bf8& b, bf8& c) {
     asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(a), "+v"(b), "+v"(c) : "n"(N));
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait_for(bf8& a) {
+    asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(a) : "n"(N));
+}
+
+// bf16 (one plane): round-to-nearest bf16 of the activations, one MFMA per step (inference).
+__device__ __forceinline__ void split1(const fx16& v, int s, bf8& hi) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) hi[j] = (__bf16)v[8 * s + j];
 }
 
 // The fragment-read / MFMA pipeline of one staged chunk, unrolled at compile time (the LDS
 // offsets are instruction immediates): reads of steps 0 and 1 first, then per step I the reads
 // of step I+2, a wait that leaves those (and step I+1's) in flight, and step I's six MFMAs.
-template <int NS>
+template <int NS, int PL>
 __device__ __forceinline__ void x6_prologue(unsigned base, bf8 (&w)[NS][3]) {
     w[0][0] = ds_read_b128_at<0 * 1024>(base);
-    w[0][1] = ds_read_b128_at<1 * 1024>(base);
-    w[0][2] = ds_read_b128_at<2 * 1024>(base);
+    if constexpr (PL == 3) {
+        w[0][1] = ds_read_b128_at<1 * 1024>(base);
+        w[0][2] = ds_read_b128_at<2 * 1024>(base);
+    }
     if constexpr (NS > 1) {
-        w[1][0] = ds_read_b128_at<3 * 1024>(base);
-        w[1][1] = ds_read_b128_at<4 * 1024>(base);
-        w[1][2] = ds_read_b128_at<5 * 1024>(base);
+        w[1][0] = ds_read_b128_at<(PL + 0) * 1024>(base);
+        if constexpr (PL == 3) {
+            w[1][1] = ds_read_b128_at<(PL + 1) * 1024>(base);
+            w[1][2] = ds_read_b128_at<(PL + 2) * 1024>(base);
+        }
     }
 }
 
@@ -304,33 +318,42 @@ __device__ __forceinline__ void tile_store_global(TileStore& ts) {
         __builtin_nontemporal_store(ts.t[q], (fx4*)(ts.dst + slab_off((lane >> 3) + 8 * q, (lane & 7) * 4)));
 }
 
-template <int NS, int NTO, int I>
+template <int NS, int NTO, int PL, int I>
 __device__ __forceinline__ void x6_step(unsigned base, bf8 (&w)[NS][3], const bf8 (&bp)[2][3],
                                         fx16 (&out)[kNT], TileStore& ts) {
     if constexpr (I < NS) {
         if constexpr (I + 2 < NS) {
-            w[I + 2][0] = ds_read_b128_at<((I + 2) * 3 + 0) * 1024>(base);
-            w[I + 2][1] = ds_read_b128_at<((I + 2) * 3 + 1) * 1024>(base);
-            w[I + 2][2] = ds_read_b128_at<((I + 2) * 3 + 2) * 1024>(base);
+            w[I + 2][0] = ds_read_b128_at<((I + 2) * PL + 0) * 1024>(base);
+            if constexpr (PL == 3) {
+                w[I + 2][1] = ds_read_b128_at<((I + 2) * PL + 1) * 1024>(base);
+                w[I + 2][2] = ds_read_b128_at<((I + 2) * PL + 2) * 1024>(base);
+            }
         }
         if constexpr (I == 0) tile_store_write(ts);
         if constexpr (I == NS / 2) tile_store_read(ts);
         if constexpr (I == NS - 1) tile_store_global(ts);
-        lgkm_wait_for<(I + 2 < NS ? 6 : (I + 1 < NS ? 3 : 0))>(w[I][0], w[I][1], w[I][2]);
         constexpr int ks = I / NTO, o = I % NTO;
-        out[o] = mfma_x6(w[I][0], w[I][1], w[I][2], bp[ks][0], bp[ks][1], bp[ks][2], out[o]);
+        constexpr int kWait = I + 2 < NS ? 2 * PL : (I + 1 < NS ? PL : 0);
+        if constexpr (PL == 3) {
+            lgkm_wait_for<kWait>(w[I][0], w[I][1], w[I][2]);
+            out[o] = mfma_x6(w[I][0], w[I][1], w[I][2], bp[ks][0], bp[ks][1], bp[ks][2], out[o]);
+        } else {
+            lgkm_wait_for<kWait>(w[I][0]);
+            out[o] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[I][0], bp[ks][0], out[o], 0, 0, 0);
+        }
         __builtin_amdgcn_sched_barrier(0);
-        x6_step<NS, NTO, I + 1>(base, w, bp, out, ts);
+        x6_step<NS, NTO, PL, I + 1>(base, w, bp, out, ts);
     }
 }
 
-template <int NTO>
+// PL = 3: bf16x6 (fp32-accurate); PL = 1: plain bf16 (one plane, one MFMA per step).
+template <int NTO, int PL>
 __device__ __forceinline__ void mma_stream_x6(const unsigned short* __restrict__ src, int nchunks,
                                               const fx16 (&in)[kNT], fx16 (&out)[kNT],
                                               unsigned char* ring, float* tstore, float* tr,
                                               const float* bias_src, float* bias_lds) {
     const int lane = threadIdx.x & 63;
-    constexpr int CB = 2 * NTO * 3 * 1024;        // bytes per chunk
+    constexpr int CB = 2 * NTO * PL * 1024;       // bytes per chunk
     constexpr int SLOT = kRingSlotBytes(true);
     stage_bytes_t<CB>(src, ring);
     if (bias_src && wave_id() == 0)
@@ -359,39 +382,45 @@ __device__ __forceinline__ void mma_stream_x6(const unsigned short* __restrict__
             const unsigned base = lds_addr(cur);
             bf8 bp[2][3];
             bf8 w[NS][3];
-            x6_prologue<NS>(base, w);
-            split3(in[c], 0, bp[0][0], bp[0][1], bp[0][2]);
-            split3(in[c], 1, bp[1][0], bp[1][1], bp[1][2]);
-            x6_step<NS, NTO, 0>(base, w, bp, out, tsx);
+            x6_prologue<NS, PL>(base, w);
+            if constexpr (PL == 3) {
+                split3(in[c], 0, bp[0][0], bp[0][1], bp[0][2]);
+                split3(in[c], 1, bp[1][0], bp[1][1], bp[1][2]);
+            } else {
+                split1(in[c], 0, bp[0][0]);
+                split1(in[c], 1, bp[1][0]);
+            }
+            x6_step<NS, NTO, PL, 0>(base, w, bp, out, tsx);
             dma_barrier();
             if (tstore && c == nchunks - 1) store_tile(in[c], tstore + c * 1024, tr);
         }
     }
 }
 
-// One layer's MMA in either precision (X6: bf16x6 split planes; else exact f32 MFMA).
-template <int NTO, bool X6>
+// One layer's MMA in the kernel's precision: PREC = bf16 planes per operand (3: bf16x6 split,
+// fp32-accurate; 1: plain bf16), PREC = 0: exact f32 MFMA.
+template <int NTO, int PREC>
 __device__ __forceinline__ void layer_mma(const FusedArgs& a, bool fwd, int l, int nchunks,
                                           const fx16 (&in)[kNT], fx16 (&out)[kNT],
                                           unsigned char* ring, float* tstore, float* tr,
                                           const float* bias_src, float* bias_lds) {
-    if (X6) {
+    if constexpr (PREC != 0) {
         const unsigned short* src = a.w6 + (fwd ? a.wf_off[l] : a.wb_off[l]);
-        mma_stream_x6<NTO>(src, nchunks, in, out, ring, tstore, tr, bias_src, bias_lds);
+        mma_stream_x6<NTO, PREC>(src, nchunks, in, out, ring, tstore, tr, bias_src, bias_lds);
     } else {
         const float* src = fwd ? a.wf + a.wf_off[l] : a.wb + a.wb_off[l];
         mma_stream_t<NTO>(src, nchunks, in, out, (float*)ring, tstore, tr, bias_src, bias_lds);
     }
 }
 
-template <bool X6>
+template <int PREC>
 __device__ __forceinline__ void layer_mma_n(const FusedArgs& a, bool fwd, int l, int nchunks, int nto,
                                             const fx16 (&in)[kNT], fx16 (&out)[kNT],
                                             unsigned char* ring, float* tstore, float* tr) {
-    if (nto <= 1) layer_mma<1, X6>(a, fwd, l, nchunks, in, out, ring, tstore, tr, nullptr, nullptr);
-    else if (nto <= 2) layer_mma<2, X6>(a, fwd, l, nchunks, in, out, ring, tstore, tr, nullptr, nullptr);
-    else if (nto <= 4) layer_mma<4, X6>(a, fwd, l, nchunks, in, out, ring, tstore, tr, nullptr, nullptr);
-    else layer_mma<8, X6>(a, fwd, l, nchunks, in, out, ring, tstore, tr, nullptr, nullptr);
+    if (nto <= 1) layer_mma<1, PREC>(a, fwd, l, nchunks, in, out, ring, tstore, tr, nullptr, nullptr);
+    else if (nto <= 2) layer_mma<2, PREC>(a, fwd, l, nchunks, in, out, ring, tstore, tr, nullptr, nullptr);
+    else if (nto <= 4) layer_mma<4, PREC>(a, fwd, l, nchunks, in, out, ring, tstore, tr, nullptr, nullptr);
+    else layer_mma<8, PREC>(a, fwd, l, nchunks, in, out, ring, tstore, tr, nullptr, nullptr);
 }
 
 // Coordinate c of sample row gs: the given point (POINTS) or o + d t in float64 (RAYS).
@@ -576,9 +605,11 @@ __device__ __forceinline__ float composite_tile(const FusedArgs& a, int wg, floa
 }
 
 // HT = output tiles of every hidden layer (widths <= 32*HT); the head has <= 32 outputs.
-// X6: bf16x6 split-plane MFMA (fp32-accurate, 2.67x the f32 MFMA rate); else exact f32 MFMA.
-template <int HT, bool X6>
+// PREC: 3 = bf16x6 split-plane MFMA (fp32-accurate, 2.67x the f32 MFMA rate), 1 = plain bf16
+// (one plane; inference), 0 = exact f32 MFMA.
+template <int HT, int PREC>
 __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs a) {
+    constexpr bool X6 = PREC != 0;   // the bf16 paths share the LDS carve
     __shared__ __attribute__((aligned(16))) unsigned char lds_raw[kLdsBytes(X6)];
     unsigned char* ring = lds_raw;
     float* ldsw = (float*)lds_raw;
@@ -665,8 +696,8 @@ __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs 
                                   : a.act + a.act_off[l - 1] + blk * (size_t)(a.kt[l] * 1024));
         float* bl = biasl + (l & 1) * (kNT * 32);
         // hidden layers l >= 1 and the head contract over HT tiles (k_l = n_{l-1})
-        if (l < a.L - 1) layer_mma<HT, X6>(a, true, l, a.kt[l], act, out, ring, ts, tr, a.bp + a.bp_off[l], bl);
-        else layer_mma<1, X6>(a, true, l, a.kt[l], act, out, ring, ts, tr, a.bp + a.bp_off[l], bl);
+        if (l < a.L - 1) layer_mma<HT, PREC>(a, true, l, a.kt[l], act, out, ring, ts, tr, a.bp + a.bp_off[l], bl);
+        else layer_mma<1, PREC>(a, true, l, a.kt[l], act, out, ring, ts, tr, a.bp + a.bp_off[l], bl);
         if (l < a.L - 1) {
 #pragma unroll
             for (int o = 0; o < HT; ++o) {
@@ -723,7 +754,7 @@ __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs 
 #pragma unroll
         for (int o = 0; o < kNT; ++o) out[o] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         float* ts = a.grad + a.grad_off[l] + blk * (size_t)(a.nt[l] * 1024);
-        layer_mma<HT, X6>(a, false, l, a.nt[l], act, out, ring, ts, tr, nullptr, nullptr);
+        layer_mma<HT, PREC>(a, false, l, a.nt[l], act, out, ring, ts, tr, nullptr, nullptr);
 #pragma unroll
         for (int o = 0; o < HT; ++o) {
 #pragma unroll
@@ -742,7 +773,7 @@ __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs 
         // also writes G_0's slab
 #pragma unroll
         for (int o = 0; o < kNT; ++o) out[o] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        layer_mma_n<X6>(a, false, 0, a.nt[0], a.kt[0], act, out, ring, g0, tr);
+        layer_mma_n<PREC>(a, false, 0, a.nt[0], a.kt[0], act, out, ring, g0, tr);
         if (valid) {
 #pragma unroll
             for (int o = 0; o < kNT; ++o)
@@ -1017,6 +1048,7 @@ struct PackArgs {
     size_t wf_off[kMaxLayers], wb_off[kMaxLayers], bp_off[kMaxLayers];
     size_t wf_n[kMaxLayers], wb_n[kMaxLayers], bp_n[kMaxLayers];
     size_t w6f_off[kMaxLayers], w6b_off[kMaxLayers], w6f_n[kMaxLayers], w6b_n[kMaxLayers];
+    int planes;                            // bf16 planes packed (3: hi/mid/lo, 1: hi)
 };
 
 __global__ void pack_kernel(PackArgs a, int l) {
@@ -1071,7 +1103,7 @@ __global__ void pack6_kernel(PackArgs a, int l) {
         const int no = fwd ? a.fo[l] : a.bo[l];
         const int j = x & 7; x >>= 3;
         const int ln = x & 63; x >>= 6;
-        const int pl = x % 3; x /= 3;
+        const int pl = x % a.planes; x /= a.planes;
         const int o = x % no; x /= no;
         const int ks = x & 1; x >>= 1;
         const int t = (int)x;
@@ -1195,7 +1227,8 @@ struct Layout {
 
 inline int pow2_tiles(int t) { return t <= 1 ? 1 : t <= 2 ? 2 : t <= 4 ? 4 : 8; }
 
-void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S) {
+// train = false (render): no slabs or dW partials (the forward-only kernel writes none).
+void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S, bool train = true) {
     const int L = m.num_layers;
     int kt[kMaxLayers], nt[kMaxLayers];
     for (int l = 0; l < L; ++l) {
@@ -1235,10 +1268,10 @@ void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S) {
     off = 0;
     y.x_off = off; off += (size_t)y.blocks * kt[0] * 1024;
     for (int l = 0; l < L - 1; ++l) { y.act_off[l] = off; off += (size_t)y.blocks * nt[l] * 1024; }
-    y.act_total = off;
+    y.act_total = train ? off : 0;
     off = 0;
     for (int l = 0; l < L; ++l) { y.grad_off[l] = off; off += (size_t)y.blocks * nt[l] * 1024; }
-    y.grad_total = off;
+    y.grad_total = train ? off : 0;
     // dW: one launch over every layer (dw_all_kernel), ~kDwGrid workgroups split between the
     // layers in proportion to the slab bytes each one streams (kt + nt tiles per 32-sample
     // block): the kernel is bandwidth-bound, so equal bytes per workgroup balance it. Phased
@@ -1265,8 +1298,8 @@ void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S) {
         dbp += (size_t)sp * nt[l] * 32;
     }
     y.dw_grid = wg;
-    y.dwp_total = dwp;
-    y.dbp_total = dbp;
+    y.dwp_total = train ? dwp : 0;
+    y.dbp_total = train ? dbp : 0;
 }
 
 }  // namespace
@@ -1291,9 +1324,9 @@ bool fused_supported(const lnerf_mlp& m, int rays, int S, int input_mode, const 
     return w == nullptr;
 }
 
-size_t fused_workspace_bytes(const lnerf_mlp& m, int rays, int S) {
+size_t fused_workspace_bytes(const lnerf_mlp& m, int rays, int S, bool train) {
     Layout y;
-    make_layout(y, m, rays, S);
+    make_layout(y, m, rays, S, train);
     size_t f = align_up(y.pack_total, 64) + align_up((y.w6_total + 1) / 2, 64) +
                align_up(y.act_total, 64) + align_up(y.grad_total, 64) +
                align_up((size_t)y.num_wg, 64) + align_up(y.dwp_total, 64) + align_up(y.dbp_total, 64) +
@@ -1301,20 +1334,22 @@ size_t fused_workspace_bytes(const lnerf_mlp& m, int rays, int S) {
     return f * sizeof(float);
 }
 
-void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws_base, int flags) {
+void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws_base, int flags,
+                bool train) {
     Layout y;
-    make_layout(y, m, b.rays, b.samples);
+    make_layout(y, m, b.rays, b.samples, train);
     p.L = m.num_layers;
     p.ht = y.ht;
     // bf16x6 keeps (L-1)*HT ReLU-mask tiles in a smaller LDS budget (the ring is 1.5x larger)
-    p.x6 = !(flags & LNERF_MFMA_F32) && (p.L - 1) * y.ht <= kMaskTiles(true);
+    const bool bf_ok = (p.L - 1) * y.ht <= kMaskTiles(true);
+    p.x6 = (flags & LNERF_MFMA_F32) || !bf_ok ? 0 : (flags & LNERF_MFMA_BF16) ? 1 : 3;
     for (int l = 0; l < p.L; ++l) {
         p.fo[l] = y.fo[l];
         p.bo[l] = y.bo[l];
         p.w6f_off[l] = y.w6f_off[l];
         p.w6b_off[l] = y.w6b_off[l];
-        p.w6f_n[l] = y.w6f_n[l];
-        p.w6b_n[l] = y.w6b_n[l];
+        p.w6f_n[l] = y.w6f_n[l] / 3 * (p.x6 ? p.x6 : 3);   // layout sized for 3 planes
+        p.w6b_n[l] = y.w6b_n[l] / 3 * (p.x6 ? p.x6 : 3);
     }
     for (int l = 0; l < p.L; ++l) {
         p.k[l] = m.k[l];
@@ -1396,6 +1431,7 @@ static void launch_pack(const FusedPlan& p, const float* ws, const float* bs, hi
     a.wb = p.wb;
     a.bp = p.bp;
     a.w6 = p.w6;
+    a.planes = p.x6;
     for (int l = 0; l < p.L; ++l) {
         if (p.x6) {
             // biases (and nothing else) through pack_kernel: bp lands after wf_n + wb_n = 0
@@ -1457,8 +1493,9 @@ static FusedArgs make_fused_args(const FusedPlan& p, const lnerf_batch& b, float
 
 static void launch_fused(const FusedPlan& p, const FusedArgs& fa, hipStream_t s) {
 #define LNERF_FUSED_LAUNCH(HT)                                                         \
-    if (p.x6) fused_fwd_bwd_kernel<HT, true><<<p.num_wg, kWgThreads, 0, s>>>(fa);      \
-    else fused_fwd_bwd_kernel<HT, false><<<p.num_wg, kWgThreads, 0, s>>>(fa);
+    if (p.x6 == 3) fused_fwd_bwd_kernel<HT, 3><<<p.num_wg, kWgThreads, 0, s>>>(fa);    \
+    else if (p.x6 == 1) fused_fwd_bwd_kernel<HT, 1><<<p.num_wg, kWgThreads, 0, s>>>(fa); \
+    else fused_fwd_bwd_kernel<HT, 0><<<p.num_wg, kWgThreads, 0, s>>>(fa);
     switch (p.ht) {
         case 1: LNERF_FUSED_LAUNCH(1) break;
         case 2: LNERF_FUSED_LAUNCH(2) break;

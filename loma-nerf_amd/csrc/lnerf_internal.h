@@ -127,7 +127,8 @@ struct FusedPlan {
     float* bp;        // biases in fragment order
     size_t wf_off[kMaxLayers], wb_off[kMaxLayers], bp_off[kMaxLayers];
     int ht;           // hidden output tiles (1/2/4/8): the fused kernel's instantiation
-    int x6;           // 1: bf16x6 split-plane MFMA; 0: exact f32 MFMA
+    int x6;           // bf16 planes per operand: 3 = bf16x6 split (fp32-accurate), 1 = bf16,
+                      // 0 = exact f32 MFMA
     int fo[kMaxLayers], bo[kMaxLayers];  // packed output tiles of each layer's fwd / bwd MMA
     unsigned short* w6;                  // bf16x6 packed planes (u16 offsets below)
     size_t w6f_off[kMaxLayers], w6b_off[kMaxLayers], w6f_n[kMaxLayers], w6b_n[kMaxLayers];
@@ -150,9 +151,11 @@ struct FusedPlan {
 };
 
 bool fused_supported(const lnerf_mlp& mlp, int rays, int S, int input_mode, const char** why);
-size_t fused_workspace_bytes(const lnerf_mlp& mlp, int rays, int S);
+// train = false sizes the forward-only (render) workspace: packed weights + loss partials.
+size_t fused_workspace_bytes(const lnerf_mlp& mlp, int rays, int S, bool train = true);
 // flags: LNERF_MFMA_F32 selects the exact f32 MFMA products over the default bf16x6 split
-void fused_plan(FusedPlan& p, const lnerf_mlp& mlp, const lnerf_batch& b, void* ws_base, int flags);
+void fused_plan(FusedPlan& p, const lnerf_mlp& mlp, const lnerf_batch& b, void* ws_base, int flags,
+                bool train = true);
 // ev: nullable array of 7 events recorded between the step's kernels (LNERF_TIMING)
 void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, const lnerf_batch& b,
                       float seed, int flags, const lnerf_outputs& out, hipStream_t s,

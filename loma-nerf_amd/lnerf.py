@@ -28,6 +28,7 @@ GENERIC = 8
 FAST = 16
 TIMING = 32
 MFMA_F32 = 64     # fused path: exact f32 MFMA instead of the bf16x6 split
+MFMA_BF16 = 128   # fused path: plain bf16 operands (reduced precision; inference)
 
 # every symbol include/lnerf.h declares (tests check the library exports all of them)
 EXPORTED_SYMBOLS = [
@@ -130,7 +131,7 @@ def configure(lib: ctypes.CDLL) -> None:
                                      ctypes.c_void_p, ctypes.POINTER(LnerfBatch), ctypes.c_float,
                                      ctypes.c_int, ctypes.POINTER(LnerfOutputs), ctypes.c_void_p]
     lib.lnerf_render.argtypes = [ctypes.c_void_p, ctypes.POINTER(LnerfMLP), ctypes.c_void_p,
-                                 ctypes.c_void_p, ctypes.POINTER(LnerfBatch),
+                                 ctypes.c_void_p, ctypes.POINTER(LnerfBatch), ctypes.c_int,
                                  ctypes.POINTER(LnerfOutputs), ctypes.c_void_p]
     lib.lnerf_scale_by_device_scalar.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
                                                  ctypes.c_void_p]
@@ -250,15 +251,19 @@ class Engine:
 
     def render(self, mlp: LnerfMLP, ws, bs, x, dists, target, *, samples: int,
                input_mode: int = INPUT_POINTS, num_freqs: int = 5, near: float = 2.0,
-               far: float = 6.0):
+               far: float = 6.0, flags: int = 0, acc=None, loss=None):
+        """Forward only (train_nerf.py:616-661 eval render): (loss, acc_color). flags may select
+        MFMA_BF16 (the config-5 inference precision), MFMA_F32 or GENERIC."""
         torch = self.torch
         rays = target.shape[0]
         b = self._batch(rays, samples, input_mode, num_freqs, x, dists, target, near, far)
-        acc = torch.empty(rays, 3, dtype=torch.float32, device=target.device)
-        loss = torch.empty(1, dtype=torch.float32, device=target.device)
+        if acc is None:
+            acc = torch.empty(rays, 3, dtype=torch.float32, device=target.device)
+        if loss is None:
+            loss = torch.empty(1, dtype=torch.float32, device=target.device)
         o = LnerfOutputs(loss.data_ptr(), acc.data_ptr(), None, None, None, None, None)
         rc = self.lib.lnerf_render(self.ctx, ctypes.byref(mlp), ws.data_ptr(), bs.data_ptr(),
-                                   ctypes.byref(b), ctypes.byref(o), self._stream())
+                                   ctypes.byref(b), flags, ctypes.byref(o), self._stream())
         if rc != 0:
             raise RuntimeError(f"lnerf_render: {last_error()}")
         return loss[0], acc

@@ -82,6 +82,28 @@ def make_batch(name="cfg3", rays=None, samples=None, rank=0):
                 rays=rays, target=target, F=F, S=S, N=N, L=L, H=H)
 
 
+def compute_psnr(img1, img2, max_val=1.0):
+    """train_nerf.py:163-183: 20 log10(max / sqrt(mean((img1 - img2)^2))), numpy or torch."""
+    mse = ((img1 - img2) ** 2).mean()
+    return 20.0 * math.log10(max_val / math.sqrt(float(mse)))
+
+
+def render_image(engine, mlp, ws, bs, width, K, c2w, samples, num_freqs, near=2.0, far=6.0,
+                 flags=0, target=None, rays=None):
+    """The eval render of train_nerf.py:558-712 on the device: get_rays for the full width x width
+    frame, sampling + encoding + MLP + compositing per ray (LNERF_INPUT_RAYS), one call.
+    Returns (width*width, 3) colours (device tensor)."""
+    import lnerf
+    if rays is None:
+        rays = engine.get_rays(width, K, c2w)
+    if target is None:
+        target = engine.torch.zeros(rays.shape[0], 3, dtype=engine.torch.float32, device=rays.device)
+    _, acc = engine.render(mlp, ws, bs, rays, None, target, samples=samples,
+                           input_mode=lnerf.INPUT_RAYS, num_freqs=num_freqs, near=near, far=far,
+                           flags=flags)
+    return acc
+
+
 def step_flops(shapes):
     """Canonical algorithmic FLOPs per sample: fwd 2KN every layer, bwd dW 2KN
     every layer, bwd dX 2KN for l >= 1."""

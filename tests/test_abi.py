@@ -137,9 +137,9 @@ def test_compat_call_without_gpu_fails_loudly():
 def test_generic_and_fused_shape_support_flags():
     # flag values are part of the ABI
     assert (lnerf.SEED_LOSS, lnerf.ACCUMULATE, lnerf.WANT_DX, lnerf.GENERIC, lnerf.FAST,
-            lnerf.TIMING, lnerf.MFMA_F32) == (1, 2, 4, 8, 16, 32, 64)
+            lnerf.TIMING, lnerf.MFMA_F32, lnerf.MFMA_BF16) == (1, 2, 4, 8, 16, 32, 64, 128)
     src = open(HEADER).read()
     for name, val in (("LNERF_SEED_LOSS", 1), ("LNERF_ACCUMULATE", 2), ("LNERF_WANT_DX", 4),
                       ("LNERF_GENERIC", 8), ("LNERF_FAST", 16), ("LNERF_TIMING", 32),
-                      ("LNERF_MFMA_F32", 64)):
+                      ("LNERF_MFMA_F32", 64), ("LNERF_MFMA_BF16", 128)):
         assert re.search(rf"{name}\s*=\s*{val}\b", src), name

@@ -340,3 +340,36 @@ def test_rays_mode_full_size_equals_points_mode(engine, full):
     assert abs(ga[0] - float(b.loss.item())) <= 1e-5 * abs(ga[0])
     assert_close("acc", ga[2], b.acc_color.cpu().numpy(), **TOL)
     assert_close("dW", ga[1], b.d_ws.cpu().numpy(), **TOL)
+
+
+# ---- eval render / config 5 ------------------------------------------------
+
+def test_render_image_bf16_close_to_fp32_accurate(engine):
+    """The full-frame eval render (get_rays + RAYS sampling + forward) at bf16 MFMA (the config-5
+    inference precision) against the fp32-accurate bf16x6 render of the same frame: PSNR of one
+    against the other stays high (bf16 keeps 8 significant bits per operand)."""
+    import lnerf
+    import scene
+    import torch
+    shapes, wp, bp = scene.init_mlp(33, 4, 8, 256)
+    mlp = lnerf.make_mlp(shapes, wp.shape[1], wp.shape[2])
+    ws, bs = _dev(engine, wp), _dev(engine, bp)
+    focal = 0.5 / np.tan(0.5 * scene.CAMERA_ANGLE_X)
+    K = np.array([[focal, 0, 0.5], [0, focal, 0.5], [0, 0, 1]])
+    c2w = scene.look_at_pose()
+    ref = scene.render_image(engine, mlp, ws, bs, 64, K, c2w, 128, 5, flags=lnerf.FAST)
+    b16 = scene.render_image(engine, mlp, ws, bs, 64, K, c2w, 128, 5,
+                             flags=lnerf.FAST | lnerf.MFMA_BF16)
+    torch.cuda.synchronize()
+    a, b = ref.cpu().numpy(), b16.cpu().numpy()
+    assert np.isfinite(b).all() and a.shape == (64 * 64, 3)
+    assert scene.compute_psnr(b, a) > 35.0, scene.compute_psnr(b, a)
+    # and the fp32-accurate render is the training forward's colours on the same rays
+    rays = engine.get_rays(64, K, c2w)
+    X, dists = _rays_reference(rays.cpu().numpy(), 128, 5)
+    import oracle
+    sub = np.arange(0, 64 * 64, 97)
+    Xs = X.reshape(64 * 64, 128, -1)[sub].reshape(-1, X.shape[1])
+    want = oracle.standard_forward_backward(Xs, wp, bp, shapes, dists[sub],
+                                            np.zeros((len(sub), 3), np.float32), 128, seed=1.0)
+    assert_close("acc", a[sub], want["acc"], **TOL)

@@ -318,10 +318,50 @@ __device__ __forceinline__ void tile_store_global(TileStore& ts) {
         __builtin_nontemporal_store(ts.t[q], (fx4*)(ts.dst + slab_off((lane >> 3) + 8 * q, (lane & 7) * 4)));
 }
 
+// The next chunk's LDS-DMA, one 4-KiB round (one 1-KiB instruction per wave) per step, so each
+// instruction's issue cost (~60 cycles, MI355X_MICROARCH.md) hides under the MFMAs instead of
+// twelve of them stalling the chunk start.
+struct ChunkDma {
+    const char* src;
+    unsigned char* dst;
+    bool on;
+};
+
+template <int CB, int R>
+__device__ __forceinline__ void chunk_dma_round(const ChunkDma& d) {
+    constexpr int kRound = kWgThreads * 16, kFull = CB / kRound, kTail = CB % kRound;
+    if constexpr (R < kFull || (R == kFull && kTail)) {
+        if (!d.on) return;
+        const int tid = threadIdx.x, wave = wave_id();
+        if (R < kFull || tid * 16 < kTail) {
+            const char* g = d.src + R * kRound + tid * 16;
+            unsigned char* l = d.dst + R * kRound + wave * 1024;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                             (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+        }
+    }
+}
+
+template <int CB, int R, int N>
+__device__ __forceinline__ void chunk_dma_rest(const ChunkDma& d) {
+    if constexpr (R < N) {
+        chunk_dma_round<CB, R>(d);
+        chunk_dma_rest<CB, R + 1, N>(d);
+    }
+}
+
 template <int NS, int NTO, int PL, int I>
 __device__ __forceinline__ void x6_step(unsigned base, bf8 (&w)[NS][3], const bf8 (&bp)[2][3],
-                                        fx16 (&out)[kNT], TileStore& ts) {
+                                        fx16 (&out)[kNT], TileStore& ts, const ChunkDma& dma) {
     if constexpr (I < NS) {
+        constexpr int CB = 2 * NTO * PL * 1024;
+        constexpr int kRounds = (CB + kWgThreads * 16 - 1) / (kWgThreads * 16);
+        // rounds spread over the steps (more rounds than steps: the rest at the last step)
+        if constexpr (I < NS - 1) {
+            chunk_dma_round<CB, I>(dma);
+        } else {
+            chunk_dma_rest<CB, I, kRounds>(dma);
+        }
         if constexpr (I + 2 < NS) {
             w[I + 2][0] = ds_read_b128_at<((I + 2) * PL + 0) * 1024>(base);
             if constexpr (PL == 3) {
@@ -342,7 +382,7 @@ __device__ __forceinline__ void x6_step(unsigned base, bf8 (&w)[NS][3], const bf
             out[o] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[I][0], bp[ks][0], out[o], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
-        x6_step<NS, NTO, PL, I + 1>(base, w, bp, out, ts);
+        x6_step<NS, NTO, PL, I + 1>(base, w, bp, out, ts, dma);
     }
 }
 
@@ -364,8 +404,10 @@ __device__ __forceinline__ void mma_stream_x6(const unsigned short* __restrict__
     for (int c = 0; c < kNT; ++c) {
         if (c < nchunks) {
             const unsigned char* cur = ring + (c & 1) * SLOT + lane * 16;
-            if (c + 1 < nchunks)
-                stage_bytes_t<CB>((const char*)src + (size_t)(c + 1) * CB, ring + ((c + 1) & 1) * SLOT);
+            ChunkDma dma;
+            dma.src = (const char*)src + (size_t)(c + 1) * CB;
+            dma.dst = ring + ((c + 1) & 1) * SLOT;
+            dma.on = c + 1 < nchunks;
             TileStore tsx;
             tsx.v = (tstore && c >= 1) ? &in[c - 1] : nullptr;
             tsx.dst = tstore + (c - 1) * 1024;
@@ -390,7 +432,7 @@ __device__ __forceinline__ void mma_stream_x6(const unsigned short* __restrict__
                 split1(in[c], 0, bp[0][0]);
                 split1(in[c], 1, bp[1][0]);
             }
-            x6_step<NS, NTO, PL, 0>(base, w, bp, out, tsx);
+            x6_step<NS, NTO, PL, 0>(base, w, bp, out, tsx, dma);
             dma_barrier();
             if (tstore && c == nchunks - 1) store_tile(in[c], tstore + c * 1024, tr);
         }

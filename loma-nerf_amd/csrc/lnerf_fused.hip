@@ -221,6 +221,21 @@ __device__ __forceinline__ void split3(const fx16& v, int s, bf8& hi, bf8& mid, 
     }
 }
 
+// One pair (elements 2q, 2q+1) of split3's k-step s: one 32-bit register of each plane.
+__device__ __forceinline__ void split3_pair(const fx16& v, int s, int q, bf8& hi, bf8& mid, bf8& lo) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const int j = 2 * q + e;
+        const float x = v[8 * s + j];
+        const __bf16 h = (__bf16)x;
+        const float r = x - (float)h;
+        const __bf16 m = (__bf16)r;
+        hi[j] = h;
+        mid[j] = m;
+        lo[j] = (__bf16)(r - (float)m);
+    }
+}
+
 __device__ __forceinline__ fx16 mfma_x6(const bf8& wh, const bf8& wm, const bf8& wl, const bf8& bh,
                                         const bf8& bm, const bf8& bl, fx16 acc) {
     // small terms first (in the order the planes arrive from LDS: hi, mid, lo)
@@ -324,14 +339,13 @@ __device__ __forceinline__ void tile_store_global(TileStore& ts) {
 struct ChunkDma {
     const char* src;
     unsigned char* dst;
-    bool on;
+    bool on;   // (unused: the rounds are unconditional, see mma_stream_x6)
 };
 
 template <int CB, int R>
 __device__ __forceinline__ void chunk_dma_round(const ChunkDma& d) {
     constexpr int kRound = kWgThreads * 16, kFull = CB / kRound, kTail = CB % kRound;
     if constexpr (R < kFull || (R == kFull && kTail)) {
-        if (!d.on) return;
         const int tid = threadIdx.x, wave = wave_id();
         if (R < kFull || tid * 16 < kTail) {
             const char* g = d.src + R * kRound + tid * 16;
@@ -351,9 +365,13 @@ __device__ __forceinline__ void chunk_dma_rest(const ChunkDma& d) {
 }
 
 template <int NS, int NTO, int PL, int I>
-__device__ __forceinline__ void x6_step(unsigned base, bf8 (&w)[NS][3], const bf8 (&bp)[2][3],
-                                        fx16 (&out)[kNT], TileStore& ts, const ChunkDma& dma) {
+__device__ __forceinline__ void x6_step(unsigned base, bf8 (&w)[NS][3], bf8 (&bp)[2][3],
+                                        fx16 (&out)[kNT], TileStore& ts, const ChunkDma& dma,
+                                        const fx16& tile) {
     if constexpr (I < NS) {
+        // the second k-step's operand split, one register pair per step under the first
+        // k-step's MFMAs (needed from step NTO on)
+        if constexpr (PL == 3 && NTO >= 4 && I < 4) split3_pair(tile, 1, I, bp[1][0], bp[1][1], bp[1][2]);
         constexpr int CB = 2 * NTO * PL * 1024;
         constexpr int kRounds = (CB + kWgThreads * 16 - 1) / (kWgThreads * 16);
         // rounds spread over the steps (more rounds than steps: the rest at the last step)
@@ -381,8 +399,7 @@ __device__ __forceinline__ void x6_step(unsigned base, bf8 (&w)[NS][3], const bf
             lgkm_wait_for<kWait>(w[I][0]);
             out[o] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[I][0], bp[ks][0], out[o], 0, 0, 0);
         }
-        __builtin_amdgcn_sched_barrier(0);
-        x6_step<NS, NTO, PL, I + 1>(base, w, bp, out, ts, dma);
+        x6_step<NS, NTO, PL, I + 1>(base, w, bp, out, ts, dma, tile);
     }
 }
 
@@ -405,9 +422,11 @@ __device__ __forceinline__ void mma_stream_x6(const unsigned short* __restrict__
         if (c < nchunks) {
             const unsigned char* cur = ring + (c & 1) * SLOT + lane * 16;
             ChunkDma dma;
-            dma.src = (const char*)src + (size_t)(c + 1) * CB;
+            // the last chunk re-stages itself into the free slot instead of branching around
+            // the per-step DMA rounds (a branch would split the step pipeline into blocks)
+            dma.src = (const char*)src + (size_t)(c + 1 < nchunks ? c + 1 : c) * CB;
             dma.dst = ring + ((c + 1) & 1) * SLOT;
-            dma.on = c + 1 < nchunks;
+            dma.on = true;
             TileStore tsx;
             tsx.v = (tstore && c >= 1) ? &in[c - 1] : nullptr;
             tsx.dst = tstore + (c - 1) * 1024;
@@ -427,12 +446,12 @@ __device__ __forceinline__ void mma_stream_x6(const unsigned short* __restrict__
             x6_prologue<NS, PL>(base, w);
             if constexpr (PL == 3) {
                 split3(in[c], 0, bp[0][0], bp[0][1], bp[0][2]);
-                split3(in[c], 1, bp[1][0], bp[1][1], bp[1][2]);
+                if constexpr (NTO < 4) split3(in[c], 1, bp[1][0], bp[1][1], bp[1][2]);
             } else {
                 split1(in[c], 0, bp[0][0]);
                 split1(in[c], 1, bp[1][0]);
             }
-            x6_step<NS, NTO, PL, 0>(base, w, bp, out, tsx, dma);
+            x6_step<NS, NTO, PL, 0>(base, w, bp, out, tsx, dma, in[c]);
             dma_barrier();
             if (tstore && c == nchunks - 1) store_tile(in[c], tstore + c * 1024, tr);
         }

@@ -18,6 +18,7 @@
 #include "lnerf_internal.h"
 
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 
 namespace lnerf {
@@ -72,7 +73,7 @@ struct FusedArgs {
 // ---- LDS carve (one __shared__ array; see cdna_hip_programming.md §5 item 4(a)) --------------
 // Weight ring: 2 slots of one contraction tile of one layer (f32: 16 regs x 8 tiles x 64 lanes x
 // 4 B = 32 KiB; bf16x6: 2 k-steps x 8 tiles x 3 planes x 64 lanes x 16 B = 48 KiB).
-// ReLU masks: one u64 ballot per (layer, tile, register) per wave, (L-1)*HT tile-layers.
+// ReLU masks: per wave and hidden layer, 64 lanes x 16 B of per-lane bits (tile, register).
 constexpr int kRingSlotBytes(bool x6) { return x6 ? 2 * kNT * 3 * 1024 : kChunkMax * 4; }
 constexpr int kMaskTiles(bool x6) { return x6 ? 64 : 120; }
 constexpr int kLdsComp = kTileSamples * kCompFloats;                    // floats
@@ -116,13 +117,35 @@ __device__ __forceinline__ void stage_bytes_t(const void* __restrict__ src, void
 // vmcnt(0), not vmcnt(N): on CDNA loads and stores share vmcnt and do not retire in order with
 // respect to each other, so a partial count cannot single out the DMA behind later stores.
 // (__syncthreads would also add lgkmcnt(0); the LDS consumers wait for their own reads.)
+// ---- optional in-kernel phase timing (build with -DLNERF_PROF=1; never in the product build):
+// per-wave s_memtime deltas accumulated in LDS by lane 0, summed into g_prof at the end.
+#ifndef LNERF_PROF
+#define LNERF_PROF 0
+#endif
+#if LNERF_PROF
+enum { kPfPE, kPfFwd, kPfWait, kPfComp, kPfBwd, kPfTail, kPfTotal, kPfFwdEpi, kPfBwdEpi, kPfN };
+__device__ unsigned long long g_prof[16];
+__device__ __forceinline__ unsigned long long* prof_slots() {
+    __shared__ unsigned long long s[kWaves][16];
+    return &s[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)][0];
+}
+#define PROF_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define PROF_ADD(cat, t0) \
+    do { if ((threadIdx.x & 63) == 0) prof_slots()[cat] += __builtin_amdgcn_s_memtime() - (t0); } while (0)
+#else
+#define PROF_T(v)
+#define PROF_ADD(cat, t0)
+#endif
+
 template <int N>
 __device__ __forceinline__ void dma_barrier_n() {
     static_assert(N == 0, "see above");
+    PROF_T(t0);
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), expcnt(7), lgkmcnt(15)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    PROF_ADD(kPfWait, t0);
 }
 __device__ __forceinline__ void dma_barrier() { dma_barrier_n<0>(); }
 
@@ -683,11 +706,16 @@ __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs 
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id(), h = lane >> 5;
     const int wg = blockIdx.x;
     const int ls = wave * 32 + (lane & 31);           // local sample 0..127
+#if LNERF_PROF
+    if (lane < kPfN) prof_slots()[lane] = 0;
+    PROF_T(t_start);
+#endif
     const int tile_samples = a.rpw * a.S;
     const int gs = wg * tile_samples + ls;            // global sample row (ray*S + j)
     const bool valid = (ls < tile_samples) && (gs < a.R);
     const size_t blk = (size_t)wg * kWaves + wave;    // 32-sample slab index
-    unsigned long long* wmask = masks + (size_t)wave * kMaskTiles(X6) * 16;   // [(l*HT + o)][16]
+    // ReLU masks, one bit per (tile, register) and lane: [layer][lane][4 x u32] per wave
+    unsigned* wmask = (unsigned*)(masks + (size_t)wave * kMaskTiles(X6) * 16);
     float* tr = trall + wave * 1024;
     const bool st = a.want_grad != 0;
 
@@ -747,8 +775,10 @@ __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs 
         __syncthreads();
     }
 
+    PROF_ADD(kPfPE, t_start);
     // ---- forward through the layers ----
     for (int l = 0; l < a.L; ++l) {
+        PROF_T(t_l);
 #pragma unroll
         for (int o = 0; o < kNT; ++o) out[o] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         // the input tiles of layer l are A_{l-1} (X for l = 0): stored while layer l computes
@@ -759,23 +789,29 @@ __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs 
         // hidden layers l >= 1 and the head contract over HT tiles (k_l = n_{l-1})
         if (l < a.L - 1) layer_mma<HT, PREC>(a, true, l, a.kt[l], act, out, ring, ts, tr, a.bp + a.bp_off[l], bl);
         else layer_mma<1, PREC>(a, true, l, a.kt[l], act, out, ring, ts, tr, a.bp + a.bp_off[l], bl);
+        PROF_ADD(kPfFwd, t_l);
+        PROF_T(t_e);
         if (l < a.L - 1) {
+            unsigned mb[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
             for (int o = 0; o < HT; ++o) {
-                unsigned long long m[16];
-                const float* bo = bl + (o * 2 + h) * 16;
+                const fx4* bq = (const fx4*)(bl + (o * 2 + h) * 16);
+                fx16 bo;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const fx4 b4 = bq[q];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) bo[4 * q + e] = b4[e];
+                }
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    float v = out[o][r] + bo[r];
-                    v = (v > 0.0f) ? v : 0.0f;               // ReLU nerf.py:141-144
-                    act[o][r] = v;
-                    m[r] = __ballot(v > 0.0f);
-                }
-                if (lane == 0) {
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) wmask[((size_t)l * HT + o) * 16 + r] = m[r];
+                    const float v = out[o][r] + bo[r];              // bias after the sum, as loma
+                    const bool pos = v > 0.0f;
+                    act[o][r] = pos ? v : 0.0f;                     // ReLU nerf.py:141-144
+                    mb[o >> 1] |= (pos ? 1u : 0u) << ((o & 1) * 16 + r);
                 }
             }
+            *(uint4*)(wmask + ((size_t)l * 64 + lane) * 4) = make_uint4(mb[0], mb[1], mb[2], mb[3]);
 #pragma unroll
             for (int o = HT; o < kNT; ++o) act[o] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         } else {
@@ -785,7 +821,9 @@ __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs 
                 for (int r = 0; r < 4; ++r) comp[ls * 4 + r] = out[0][r] + bl[r];  // c_z[ls][r]
             }
         }
+        PROF_ADD(kPfFwdEpi, t_e);
     }
+    PROF_T(t_c);
     __syncthreads();
 
     // ---- rendering + loss + rendering reverse: one thread per sample, scans along rays ----
@@ -797,6 +835,7 @@ __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs 
         for (int r = 0; r < a.rpw; ++r) l = l + rayloss[r];
         a.loss_part[wg] = l;
     }
+    PROF_ADD(kPfComp, t_c);
     if (!a.want_grad) return;
 
     // ---- reverse chain: G_{L-1} from the head, then G_{l-1} = (W_l G_l) * 1[A_{l-1} > 0] ----
@@ -812,21 +851,26 @@ __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs 
     (void)g;
     (void)go;
     for (int l = a.L - 1; l >= 1; --l) {
+        PROF_T(t_b);
 #pragma unroll
         for (int o = 0; o < kNT; ++o) out[o] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         float* ts = a.grad + a.grad_off[l] + blk * (size_t)(a.nt[l] * 1024);
         layer_mma<HT, PREC>(a, false, l, a.nt[l], act, out, ring, ts, tr, nullptr, nullptr);
+        PROF_ADD(kPfBwd, t_b);
+        PROF_T(t_be);
+        const uint4 mq = *(const uint4*)(wmask + ((size_t)(l - 1) * 64 + lane) * 4);
+        const unsigned mb[4] = {mq.x, mq.y, mq.z, mq.w};
 #pragma unroll
         for (int o = 0; o < HT; ++o) {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const unsigned long long m = wmask[((size_t)(l - 1) * HT + o) * 16 + r];
-                act[o][r] = ((m >> lane) & 1ull) ? out[o][r] : 0.0f;
-            }
+            for (int r = 0; r < 16; ++r)
+                act[o][r] = ((mb[o >> 1] >> ((o & 1) * 16 + r)) & 1u) ? out[o][r] : 0.0f;
         }
 #pragma unroll
         for (int o = HT; o < kNT; ++o) act[o] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        PROF_ADD(kPfBwdEpi, t_be);
     }
+    PROF_T(t_t);
     // act now holds G_0 (nt[0] tiles)
     float* g0 = a.grad + a.grad_off[0] + blk * (size_t)(a.nt[0] * 1024);
     if (a.d_x) {
@@ -851,6 +895,11 @@ __global__ void __launch_bounds__(kWgThreads, 1) fused_fwd_bwd_kernel(FusedArgs 
         for (int o = 0; o < kNT; ++o)
             if (o < a.nt[0]) store_tile(act[o], g0 + o * 1024, tr);
     }
+#if LNERF_PROF
+    PROF_ADD(kPfTail, t_t);
+    PROF_ADD(kPfTotal, t_start);
+    if (lane < kPfN) atomicAdd(&g_prof[lane], prof_slots()[lane]);
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1402,7 +1451,8 @@ void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws
     p.L = m.num_layers;
     p.ht = y.ht;
     // bf16x6 keeps (L-1)*HT ReLU-mask tiles in a smaller LDS budget (the ring is 1.5x larger)
-    const bool bf_ok = (p.L - 1) * y.ht <= kMaskTiles(true);
+    // per-lane ReLU masks take 1 KiB per hidden layer and wave: (L-1) <= kMaskTiles / 8
+    const bool bf_ok = (p.L - 1) <= kMaskTiles(true) / 8;
     p.x6 = (flags & LNERF_MFMA_F32) || !bf_ok ? 0 : (flags & LNERF_MFMA_BF16) ? 1 : 3;
     for (int l = 0; l < p.L; ++l) {
         p.fo[l] = y.fo[l];
@@ -1566,6 +1616,22 @@ static void launch_fused(const FusedPlan& p, const FusedArgs& fa, hipStream_t s)
 #undef LNERF_FUSED_LAUNCH
 }
 
+#if LNERF_PROF
+static void prof_report(const FusedPlan& p, hipStream_t s) {
+    unsigned long long h[16] = {};
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_prof), sizeof(h));
+    const char* names[] = {"pe", "fwd_mma", "barrier_wait", "composite", "bwd_mma", "tail",
+                           "total", "fwd_epilogue", "bwd_epilogue"};
+    const double waves = (double)p.num_wg * kWaves;
+    fprintf(stderr, "LNERF_PROF per-wave cycles:");
+    for (int i = 0; i < kPfN; ++i) fprintf(stderr, " %s=%.0f", names[i], h[i] / waves);
+    fprintf(stderr, "\n");
+    unsigned long long z[16] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z));
+}
+#endif
+
 void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, const lnerf_batch& b,
                       float seed, int flags, const lnerf_outputs& out, hipStream_t s,
                       hipEvent_t* ev) {
@@ -1578,6 +1644,9 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
     mark(1);
     FusedArgs fa = make_fused_args(p, b, seed_loss ? 1.0f : seed, out, true);
     launch_fused(p, fa, s);
+#if LNERF_PROF
+    prof_report(p, s);
+#endif
     mark(2);
     loss_reduce_kernel<<<1, 256, 0, s>>>(p.loss_part, p.num_wg, p.loss_total, out.loss);
     mark(3);

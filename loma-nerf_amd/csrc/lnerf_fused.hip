@@ -122,8 +122,15 @@ __device__ __forceinline__ void stage_bytes_t(const void* __restrict__ src, void
 #ifndef LNERF_PROF
 #define LNERF_PROF 0
 #endif
+#ifndef LNERF_PROF_NOSTORE   // profiling experiments only: drop the slab stores / weight DMA
+#define LNERF_PROF_NOSTORE 0
+#endif
+#ifndef LNERF_PROF_NODMA
+#define LNERF_PROF_NODMA 0
+#endif
 #if LNERF_PROF
-enum { kPfPE, kPfFwd, kPfWait, kPfComp, kPfBwd, kPfTail, kPfTotal, kPfFwdEpi, kPfBwdEpi, kPfN };
+enum { kPfPE, kPfFwd, kPfWait, kPfComp, kPfBwd, kPfTail, kPfTotal, kPfFwdEpi, kPfBwdEpi,
+       kPfChunkPro, kPfSteps, kPfLastStore, kPfN };
 __device__ unsigned long long g_prof[16];
 __device__ __forceinline__ unsigned long long* prof_slots() {
     __shared__ unsigned long long s[kWaves][16];
@@ -368,7 +375,7 @@ struct ChunkDma {
 template <int CB, int R>
 __device__ __forceinline__ void chunk_dma_round(const ChunkDma& d) {
     constexpr int kRound = kWgThreads * 16, kFull = CB / kRound, kTail = CB % kRound;
-    if constexpr (R < kFull || (R == kFull && kTail)) {
+    if constexpr (!LNERF_PROF_NODMA && (R < kFull || (R == kFull && kTail))) {
         const int tid = threadIdx.x, wave = wave_id();
         if (R < kFull || tid * 16 < kTail) {
             const char* g = d.src + R * kRound + tid * 16;
@@ -443,6 +450,7 @@ __device__ __forceinline__ void mma_stream_x6(const unsigned short* __restrict__
 #pragma unroll
     for (int c = 0; c < kNT; ++c) {
         if (c < nchunks) {
+            PROF_T(t_cp);
             const unsigned char* cur = ring + (c & 1) * SLOT + lane * 16;
             ChunkDma dma;
             // the last chunk re-stages itself into the free slot instead of branching around
@@ -451,7 +459,7 @@ __device__ __forceinline__ void mma_stream_x6(const unsigned short* __restrict__
             dma.dst = ring + ((c + 1) & 1) * SLOT;
             dma.on = true;
             TileStore tsx;
-            tsx.v = (tstore && c >= 1) ? &in[c - 1] : nullptr;
+            tsx.v = (tstore && c >= 1 && !LNERF_PROF_NOSTORE) ? &in[c - 1] : nullptr;
             tsx.dst = tstore + (c - 1) * 1024;
             tsx.tr = tr;
             // retire any scalar (kernarg) loads still in flight: while one is pending the
@@ -474,9 +482,14 @@ __device__ __forceinline__ void mma_stream_x6(const unsigned short* __restrict__
                 split1(in[c], 0, bp[0][0]);
                 split1(in[c], 1, bp[1][0]);
             }
+            PROF_ADD(kPfChunkPro, t_cp);
+            PROF_T(t_st);
             x6_step<NS, NTO, PL, 0>(base, w, bp, out, tsx, dma, in[c]);
+            PROF_ADD(kPfSteps, t_st);
             dma_barrier();
+            PROF_T(t_ls);
             if (tstore && c == nchunks - 1) store_tile(in[c], tstore + c * 1024, tr);
+            PROF_ADD(kPfLastStore, t_ls);
         }
     }
 }
@@ -1622,7 +1635,8 @@ static void prof_report(const FusedPlan& p, hipStream_t s) {
     (void)hipStreamSynchronize(s);
     (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_prof), sizeof(h));
     const char* names[] = {"pe", "fwd_mma", "barrier_wait", "composite", "bwd_mma", "tail",
-                           "total", "fwd_epilogue", "bwd_epilogue"};
+                           "total", "fwd_epilogue", "bwd_epilogue", "chunk_prologue", "steps",
+                           "last_store"};
     const double waves = (double)p.num_wg * kWaves;
     fprintf(stderr, "LNERF_PROF per-wave cycles:");
     for (int i = 0; i < kPfN; ++i) fprintf(stderr, " %s=%.0f", names[i], h[i] / waves);

@@ -125,12 +125,15 @@ __device__ __forceinline__ void stage_bytes_t(const void* __restrict__ src, void
 #ifndef LNERF_PROF_NOSTORE   // profiling experiments only: drop the slab stores / weight DMA
 #define LNERF_PROF_NOSTORE 0
 #endif
+#ifndef LNERF_X6P   // 1: hand-placed bf16x6 step pipeline (mma_stream_x6p); 0: compiler-scheduled
+#define LNERF_X6P 1
+#endif
 #ifndef LNERF_PROF_NODMA
 #define LNERF_PROF_NODMA 0
 #endif
 #if LNERF_PROF
 enum { kPfPE, kPfFwd, kPfWait, kPfComp, kPfBwd, kPfTail, kPfTotal, kPfFwdEpi, kPfBwdEpi,
-       kPfChunkPro, kPfSteps, kPfLastStore, kPfN };
+       kPfChunkPro, kPfSteps, kPfLastStore, kPfLayerPro, kPfChunkBar, kPfN };
 __device__ unsigned long long g_prof[16];
 __device__ __forceinline__ unsigned long long* prof_slots() {
     __shared__ unsigned long long s[kWaves][16];
@@ -394,6 +397,304 @@ __device__ __forceinline__ void chunk_dma_rest(const ChunkDma& d) {
     }
 }
 
+// ---- bf16x6 step pipeline with hand-placed fillers -------------------------------------------
+// One wave per SIMD issues in order, and a v_mfma_f32_32x32x16_bf16 gap hides about 24 cycles of
+// other issue (MI355X_MICROARCH.md, cycle constants): the six dependent MFMAs of a step leave six
+// gaps, and each filler (an LDS-DMA round, a fragment read, half of an operand-pair split, a piece
+// of the slab-tile transpose or store) is pinned into one of them with sched_barrier. Every LDS op
+// inside the pipeline is inline asm counted by hand, so each step waits for exactly its own
+// fragments (lgkmcnt, in-order LDS completion; no SMEM may be outstanding: flushed per layer).
+//
+// Per chunk c (NS = 2 NTO steps; step I = k-step I / NTO, output tile I % NTO):
+//   G1 (after MFMA 1)  LDS-DMA round(s) of chunk c+1 (steps 0..NS-2)
+//   G2, G3             fragment reads of step I+2 (planes 0, 1) + halves of an operand-pair split
+//                      (k-step 1 of this chunk during steps 0..3, k-step 0 of chunk c+1 during
+//                      steps NTO..NTO+3)
+//   G4                 fragment read of step I+2 (plane 2)
+//   G5, G6             slab tile of input tile c-1: LDS transpose writes (steps 0, 1), transposed
+//                      reads (step 2), buffer stores (step 5: early, so their write acks are back
+//                      before the chunk-end barrier's vmcnt(0))
+//   step NS-1          after its wait: vmcnt(0) + s_barrier (chunk c+1 landed; every wave has
+//                      read all of chunk c), then in G6 the fragment reads of chunk c+1's steps 0, 1.
+template <int NS>
+struct X6Sched {
+    static constexpr bool kWide = NS >= 8;
+    static constexpr int kWrA = 0, kWrB = kWide ? 1 : 0, kRd = kWide ? 2 : 1;
+    static constexpr int kGl = kWide ? 5 : NS - 1;
+    static constexpr int tile_ops(int I, bool tile) {
+        return !tile || LNERF_PROF_NOSTORE == 3 ? 0 : kWide ? (I <= 1 ? 8 : I == 2 ? 4 : 0) : (I == 0 ? 16 : I == 1 ? 4 : 0);
+    }
+    static constexpr int reads(int I) { return I + 2 < NS ? 3 : 0; }
+    // LDS ops issued after the last fragment read of step I, before step I's wait
+    static constexpr int wait(int I, bool tile) {
+        const int n = I == 0 ? 3
+                      : I == 1 ? reads(0) + tile_ops(0, tile)
+                               : tile_ops(I - 2, tile) + reads(I - 1) + tile_ops(I - 1, tile);
+        return n > 15 ? 15 : n;
+    }
+};
+
+typedef unsigned int ux4 __attribute__((ext_vector_type(4)));
+
+template <int OFF>
+__device__ __forceinline__ void ds_write_b32_at(unsigned addr, float v) {
+    asm volatile("ds_write_b32 %0, %1 offset:%2" : : "v"(addr), "v"(v), "n"(OFF));
+}
+template <int OFF>
+__device__ __forceinline__ fx4 ds_read_b128_f4(unsigned addr) {
+    fx4 r;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+    return r;
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait_t(fx4 (&t)[4]) {
+    asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]) : "n"(N));
+}
+
+#define X6_SB() __builtin_amdgcn_sched_barrier(0)
+
+// One half of split3_pair: A = hi plane and first remainder, B = mid and lo planes.
+struct PairSplit {
+    float r0, r1;
+};
+__device__ __forceinline__ void split_pair_a(const fx16& v, int s, int q, bf8& hi, PairSplit& ps) {
+    const float x0 = v[8 * s + 2 * q], x1 = v[8 * s + 2 * q + 1];
+    const __bf16 h0 = (__bf16)x0, h1 = (__bf16)x1;
+    hi[2 * q] = h0;
+    hi[2 * q + 1] = h1;
+    ps.r0 = x0 - (float)h0;
+    ps.r1 = x1 - (float)h1;
+}
+__device__ __forceinline__ void split_pair_b(int q, const PairSplit& ps, bf8& mid, bf8& lo) {
+    const __bf16 m0 = (__bf16)ps.r0, m1 = (__bf16)ps.r1;
+    mid[2 * q] = m0;
+    mid[2 * q + 1] = m1;
+    lo[2 * q] = (__bf16)(ps.r0 - (float)m0);
+    lo[2 * q + 1] = (__bf16)(ps.r1 - (float)m1);
+}
+
+struct X6Pipe {
+    unsigned base;             // this lane's fragment address in the current chunk's slot
+    unsigned nbase;            // ... in the next chunk's slot
+    unsigned trw, trr;         // transpose tile: write address (lane = sample), read address
+    const fx16* tile;          // input tile c-1 (slab store) or nullptr (compile-time per chunk)
+    const fx16* cur;           // input tile c (k-step 1 split)
+    const fx16* next;          // input tile c+1 (k-step 0 split)
+    __amdgpu_buffer_rsrc_t rsrc;   // slab of this layer and block (num_records 0: no store)
+    int voff, soff;            // buffer store offsets (lane part, chunk part), bytes
+    ChunkDma dma;
+    fx4 t[4];                  // transposed tile, in flight from step kRd to kGl
+    PairSplit ps;
+};
+
+template <int NS, int NTO, bool TILE, int I, int G>
+__device__ __forceinline__ void x6p_tile_piece(X6Pipe& p) {
+    using S = X6Sched<NS>;
+    if constexpr (TILE && LNERF_PROF_NOSTORE != 3) {
+        // transpose writes: 4 (wide) or 8 registers per gap
+        constexpr int kPer = S::kWide ? 4 : 8;
+        constexpr int kFirst = S::kWide ? ((I == S::kWrA ? 0 : 8) + (G == 5 ? 0 : 4)) : (G == 5 ? 0 : 8);
+        if constexpr ((I == S::kWrA || I == S::kWrB) && (S::kWide || I == 0)) {
+            if constexpr (kFirst + kPer <= 16) {
+#define X6_TRW(r) ds_write_b32_at<(((r) & 3) + 8 * ((r) >> 2)) * 128>(p.trw, (*p.tile)[r])
+                if constexpr (kFirst + 0 < 16) X6_TRW(kFirst + 0);
+                if constexpr (kFirst + 1 < 16) X6_TRW(kFirst + 1);
+                if constexpr (kFirst + 2 < 16) X6_TRW(kFirst + 2);
+                if constexpr (kFirst + 3 < 16) X6_TRW(kFirst + 3);
+                if constexpr (kPer == 8) {
+                    X6_TRW(kFirst + 4);
+                    X6_TRW(kFirst + 5);
+                    X6_TRW(kFirst + 6);
+                    X6_TRW(kFirst + 7);
+                }
+#undef X6_TRW
+            }
+        }
+        if constexpr (I == S::kRd && G == 5) {
+            p.t[0] = ds_read_b128_f4<0>(p.trr);
+            p.t[1] = ds_read_b128_f4<1024>(p.trr);
+            if constexpr (!S::kWide) {
+                p.t[2] = ds_read_b128_f4<2048>(p.trr);
+                p.t[3] = ds_read_b128_f4<3072>(p.trr);
+            }
+        }
+        if constexpr (S::kWide && I == S::kRd && G == 6) {
+            p.t[2] = ds_read_b128_f4<2048>(p.trr);
+            p.t[3] = ds_read_b128_f4<3072>(p.trr);
+        }
+    }
+    if constexpr (TILE && LNERF_PROF_NOSTORE != 2) {
+        if constexpr (I == S::kGl) {
+            if constexpr (!S::kWide && G == 6) lgkm_wait_t<0>(p.t);
+            constexpr int q0 = S::kWide ? (G == 5 ? 0 : 2) : 0, nq = S::kWide ? 2 : (G == 6 ? 4 : 0);
+#pragma unroll
+            for (int q = q0; q < q0 + nq; ++q)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ux4, p.t[q]), p.rsrc,
+                                                       p.voff + 512 * q, p.soff, 2 /* nt */);
+        }
+    }
+}
+
+#ifndef LNERF_X6P_DMA_GAP
+#define LNERF_X6P_DMA_GAP 1
+#endif
+// the LDS-DMA round(s) of step I, in gap G = LNERF_X6P_DMA_GAP
+template <int NS, int NTO, int I, int G>
+__device__ __forceinline__ void x6p_dma(X6Pipe& p) {
+    constexpr int CB = 2 * NTO * 3 * 1024;
+    constexpr int kRounds = (CB + kWgThreads * 16 - 1) / (kWgThreads * 16);
+    if constexpr (G == LNERF_X6P_DMA_GAP && I < NS - 1) {
+        if constexpr (I < NS - 2) {
+            chunk_dma_round<CB, I>(p.dma);
+        } else {
+            chunk_dma_rest<CB, I, kRounds>(p.dma);
+        }
+    }
+}
+
+template <int NS, int NTO, bool TILE, int I>
+__device__ __forceinline__ void x6p_step(X6Pipe& p, bf8 (&w)[NS][3], bf8 (&bp)[2][3], fx16 (&out)[kNT]) {
+    if constexpr (I < NS) {
+        using S = X6Sched<NS>;
+        constexpr int ks = I / NTO, o = I % NTO;
+        constexpr int kW = S::wait(I, TILE);
+        if constexpr (TILE && I == S::kGl && S::kWide) lgkm_wait_t<kW>(p.t);
+        lgkm_wait_for<kW>(w[I][0], w[I][1], w[I][2]);
+        if constexpr (I == NS - 1) {
+            // chunk c+1 has landed (this wave's DMA) and, after the barrier, every wave's; every
+            // wave has also finished reading chunk c, so its slot may be overwritten from here on
+            PROF_T(t_b);
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            PROF_ADD(kPfChunkBar, t_b);
+        }
+        X6_SB();
+        // G1 .. G6 (see above)
+        out[o] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[I][0], bp[ks][2], out[o], 0, 0, 0);
+        X6_SB();
+        x6p_dma<NS, NTO, I, 1>(p);
+        X6_SB();
+        out[o] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[I][1], bp[ks][1], out[o], 0, 0, 0);
+        X6_SB();
+        x6p_dma<NS, NTO, I, 2>(p);
+        if constexpr (I + 2 < NS) w[I + 2][0] = ds_read_b128_at<((I + 2) * 3 + 0) * 1024>(p.base);
+        if constexpr (NTO >= 4 && I < 4) split_pair_a(*p.cur, 1, I, bp[1][0], p.ps);
+        if constexpr (NTO >= 4 && I >= NTO && I < NTO + 4) split_pair_a(*p.next, 0, I - NTO, bp[0][0], p.ps);
+        X6_SB();
+        out[o] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[I][2], bp[ks][0], out[o], 0, 0, 0);
+        X6_SB();
+        if constexpr (I + 2 < NS) w[I + 2][1] = ds_read_b128_at<((I + 2) * 3 + 1) * 1024>(p.base);
+        if constexpr (NTO >= 4 && I < 4) split_pair_b(I, p.ps, bp[1][1], bp[1][2]);
+        if constexpr (NTO >= 4 && I >= NTO && I < NTO + 4) split_pair_b(I - NTO, p.ps, bp[0][1], bp[0][2]);
+        X6_SB();
+        out[o] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[I][1], bp[ks][0], out[o], 0, 0, 0);
+        X6_SB();
+        x6p_dma<NS, NTO, I, 4>(p);
+        if constexpr (I + 2 < NS) w[I + 2][2] = ds_read_b128_at<((I + 2) * 3 + 2) * 1024>(p.base);
+        X6_SB();
+        out[o] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[I][0], bp[ks][1], out[o], 0, 0, 0);
+        X6_SB();
+        x6p_dma<NS, NTO, I, 5>(p);
+        x6p_tile_piece<NS, NTO, TILE, I, 5>(p);
+        X6_SB();
+        out[o] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[I][0], bp[ks][0], out[o], 0, 0, 0);
+        X6_SB();
+        x6p_dma<NS, NTO, I, 6>(p);
+        x6p_tile_piece<NS, NTO, TILE, I, 6>(p);
+        if constexpr (I == NS - 1) {
+            // chunk c+1's first two steps (the last chunk reads its re-staged copy; unused)
+            w[0][0] = ds_read_b128_at<0 * 1024>(p.nbase);
+            w[0][1] = ds_read_b128_at<1 * 1024>(p.nbase);
+            w[0][2] = ds_read_b128_at<2 * 1024>(p.nbase);
+            w[1][0] = ds_read_b128_at<3 * 1024>(p.nbase);
+            w[1][1] = ds_read_b128_at<4 * 1024>(p.nbase);
+            w[1][2] = ds_read_b128_at<5 * 1024>(p.nbase);
+        }
+        X6_SB();
+        x6p_step<NS, NTO, TILE, I + 1>(p, w, bp, out);
+    }
+}
+
+// bf16x6 layer stream on the hand-placed pipeline (see X6Sched).
+template <int NTO>
+__device__ __forceinline__ void mma_stream_x6p(const unsigned short* __restrict__ src, int nchunks,
+                                               const fx16 (&in)[kNT], fx16 (&out)[kNT],
+                                               unsigned char* ring, float* tstore, float* tr,
+                                               const float* bias_src, float* bias_lds) {
+    PROF_T(t_lp);
+    const int lane = threadIdx.x & 63;
+    constexpr int NS = 2 * NTO;
+    constexpr int CB = 2 * NTO * 3 * 1024;
+    constexpr int SLOT = kRingSlotBytes(true);
+    stage_bytes_t<CB>(src, ring);
+    if (bias_src && wave_id() == 0)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bias_src + lane * 4),
+                                         (__attribute__((address_space(3))) void*)bias_lds, 16, 0, 0);
+    X6Pipe p;
+    const int h = lane >> 5, sl = lane & 31;
+    p.trw = lds_addr(tr) + (unsigned)((4 * h * 32 + sl) * 4);
+    p.trr = lds_addr(tr) + (unsigned)(((lane >> 3) * 32 + (lane & 7) * 4) * 4);
+    p.voff = (((lane & 7) >> 2) * 512 + (lane >> 3) * 16 + (lane & 3) * 4) * 4;
+    p.rsrc = __builtin_amdgcn_make_buffer_rsrc(tstore, 0, tstore ? nchunks * 4096 : 0, 0x00020000);
+    bf8 bp[2][3];
+    bf8 w[NS][3];
+    dma_barrier();
+    // no scalar load may be in flight inside the pipeline (see X6Sched)
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+    X6_SB();
+    {
+        const unsigned b0 = lds_addr(ring) + lane * 16;
+        w[0][0] = ds_read_b128_at<0 * 1024>(b0);
+        w[0][1] = ds_read_b128_at<1 * 1024>(b0);
+        w[0][2] = ds_read_b128_at<2 * 1024>(b0);
+        w[1][0] = ds_read_b128_at<3 * 1024>(b0);
+        w[1][1] = ds_read_b128_at<4 * 1024>(b0);
+        w[1][2] = ds_read_b128_at<5 * 1024>(b0);
+    }
+    split3(in[0], 0, bp[0][0], bp[0][1], bp[0][2]);
+    X6_SB();
+    PROF_ADD(kPfLayerPro, t_lp);
+#pragma unroll
+    for (int c = 0; c < kNT; ++c) {
+        if (c < nchunks) {
+            PROF_T(t_st);
+            p.base = lds_addr(ring + (c & 1) * SLOT) + lane * 16;
+            p.nbase = lds_addr(ring + ((c + 1) & 1) * SLOT) + lane * 16;
+            // the last chunk re-stages itself into the free slot instead of branching around
+            // the per-step DMA rounds (a branch would split the step pipeline into blocks)
+            p.dma.src = (const char*)src + (size_t)(c + 1 < nchunks ? c + 1 : c) * CB;
+            p.dma.dst = ring + ((c + 1) & 1) * SLOT;
+            p.dma.on = true;
+            p.cur = &in[c];
+            p.tile = c >= 1 ? &in[c - 1] : nullptr;
+            // k-step 0 operand of chunk c+1, split under chunk c (junk, unused, after the last)
+            p.next = &in[c + 1 < kNT ? c + 1 : c];
+            p.soff = (c - 1) * 4096;
+            if constexpr (NTO < 4) {
+                split3(in[c], 1, bp[1][0], bp[1][1], bp[1][2]);
+                X6_SB();
+            }
+            if (c >= 1 && LNERF_PROF_NOSTORE != 1) {
+                x6p_step<NS, NTO, true, 0>(p, w, bp, out);
+            } else {
+                x6p_step<NS, NTO, false, 0>(p, w, bp, out);
+            }
+            if constexpr (NTO < 4) {
+                split3(*p.next, 0, bp[0][0], bp[0][1], bp[0][2]);
+            }
+            PROF_ADD(kPfSteps, t_st);
+            PROF_T(t_ls);
+            if (tstore && c == nchunks - 1) {
+                __builtin_amdgcn_s_waitcnt(0xC07F);
+                store_tile(in[c], tstore + c * 1024, tr);
+            }
+            PROF_ADD(kPfLastStore, t_ls);
+        }
+    }
+}
+
 template <int NS, int NTO, int PL, int I>
 __device__ __forceinline__ void x6_step(unsigned base, bf8 (&w)[NS][3], bf8 (&bp)[2][3],
                                         fx16 (&out)[kNT], TileStore& ts, const ChunkDma& dma,
@@ -439,6 +740,12 @@ __device__ __forceinline__ void mma_stream_x6(const unsigned short* __restrict__
                                               const fx16 (&in)[kNT], fx16 (&out)[kNT],
                                               unsigned char* ring, float* tstore, float* tr,
                                               const float* bias_src, float* bias_lds) {
+#if LNERF_X6P
+    if constexpr (PL == 3) {
+        mma_stream_x6p<NTO>(src, nchunks, in, out, ring, tstore, tr, bias_src, bias_lds);
+        return;
+    }
+#endif
     const int lane = threadIdx.x & 63;
     constexpr int CB = 2 * NTO * PL * 1024;       // bytes per chunk
     constexpr int SLOT = kRingSlotBytes(true);
@@ -1636,7 +1943,7 @@ static void prof_report(const FusedPlan& p, hipStream_t s) {
     (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_prof), sizeof(h));
     const char* names[] = {"pe", "fwd_mma", "barrier_wait", "composite", "bwd_mma", "tail",
                            "total", "fwd_epilogue", "bwd_epilogue", "chunk_prologue", "steps",
-                           "last_store"};
+                           "last_store", "layer_prologue", "chunk_barrier"};
     const double waves = (double)p.num_wg * kWaves;
     fprintf(stderr, "LNERF_PROF per-wave cycles:");
     for (int i = 0; i < kPfN; ++i) fprintf(stderr, " %s=%.0f", names[i], h[i] / waves);

@@ -14,7 +14,8 @@ import os
 from dataclasses import dataclass
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libloma_nerf.so")
+# LNERF_LIB: an alternative in-tree build (e.g. the LNERF_PROF phase-counter variant)
+LIB_PATH = os.environ.get("LNERF_LIB") or os.path.join(HERE, "lib", "libloma_nerf.so")
 MAX_LAYERS = 16
 
 INPUT_ENCODED = 0

@@ -1,0 +1,200 @@
+// lnerf_composite.h -- per-sample input features and the per-tile compositing (forward,
+// loss, reverse) shared by the fused kernels (lnerf_fused.hip, lnerf_k16.hip). Templates over the
+// kernel's argument struct (fields: input_mode, x, S, k0, near_t, far_t, rays, rpw, dists,
+// target, acc_color, seed, d_target, d_dists). A tile is 128 samples of whole rays; threads
+// 0..127 own one sample each, every other thread of the workgroup only joins the barriers.
+#pragma once
+#include "lnerf_internal.h"
+
+namespace lnerf {
+namespace comp {
+
+constexpr int kTileSamples = 128;
+constexpr int kCompFloats = 24;            // per-sample compositing scratch floats in LDS
+
+// Coordinate c of sample row gs: the given point (POINTS) or o + d t in float64 (RAYS).
+template <class A>
+__device__ __forceinline__ double sample_coord(const A& a, int gs, int c) {
+    if (a.input_mode == LNERF_INPUT_RAYS) {
+        const int ray = gs / a.S, j = gs - ray * a.S;
+        return ray_point(a.x + (size_t)ray * 6, c, j, a.S, a.near_t, a.far_t);
+    }
+    return (double)a.x[(size_t)gs * 3 + c];
+}
+
+template <class A>
+__device__ __forceinline__ float input_feature(const A& a, int gs, bool valid, int f) {
+    if (!valid || f >= a.k0) return 0.0f;
+    if (a.input_mode == LNERF_INPUT_ENCODED) return a.x[(size_t)gs * a.k0 + f];
+    // positional_encoding_3d (pos_encoding.py:54-66): block-major, float64 trig, rounded once
+    const int c = f % 3, blk = f / 3;
+    const double xc = sample_coord(a, gs, c);
+    if (blk == 0) return (float)xc;
+    const int fb = blk - 1, freq = fb >> 1;
+    const double arg = ldexp(xc, freq);
+    return (fb & 1) ? (float)cos(arg) : (float)sin(arg);
+}
+
+// ---- rendering (nerf.py:176-302), loss and its reverse for one 128-sample tile ----------------
+// One thread per sample (threads 0..127; a ray = S consecutive samples = one scan segment), the
+// along-ray dependencies as segmented Hillis-Steele scans in LDS (log2 S rounds):
+//   forward  P_j = prod_{i<=j} c_i (inclusive, T_0 = 1, T_j = P_j: nerf.py:226-272),
+//            C = sum_j w_j rgb_j (segmented sum, read at the ray's last sample);
+//   reverse  G_j = a_j + c_{j+1} G_{j+1} (the reverse of the inclusive cumprod,
+//            a_j = alpha_j dL/dw_j for j >= 1), dc_j = P_{j-1} G_j, dc_0 = G_0.
+// Every per-sample expression is loma's (composite rules of lnerf_generic.hip); only the
+// association of the along-ray products and sums differs from loma's sequential loops, at fp32
+// rounding level (the parity tolerance covers it; the generic path keeps the exact order).
+// LDS: comp[0..512) z [128][4] (in), [512..1024) gz [128][4] (out), two [4][128] ping-pong scan
+// buffers at 1024 / 1536, P at 2048, per-ray dacc [128][4] at 2176 (kCompFloats = 24 per sample).
+__device__ __forceinline__ void seg_scan_fwd(float* buf0, float* buf1, int ls, int j, int S, int nv,
+                                             float (&v)[4], bool prod_first) {
+    // inclusive segmented scan of nv values (v[0] by product if prod_first, the rest by sum)
+    float* cur = buf0;
+    float* nxt = buf1;
+    for (int d = 1; d < S; d <<= 1) {
+        if (ls < kTileSamples)
+            for (int q = 0; q < nv; ++q) cur[q * kTileSamples + ls] = v[q];
+        __syncthreads();
+        if (ls < kTileSamples && j >= d) {
+            for (int q = 0; q < nv; ++q) {
+                const float o = cur[q * kTileSamples + ls - d];
+                v[q] = (q == 0 && prod_first) ? o * v[q] : o + v[q];
+            }
+        }
+        float* t = cur;
+        cur = nxt;
+        nxt = t;
+    }
+    __syncthreads();   // the next scan may write the buffer this one read last
+}
+
+template <class A>
+__device__ __forceinline__ float composite_tile(const A& a, int wg, float* comp, float* rayloss,
+                                                bool grad) {
+    const int tid = threadIdx.x, S = a.S;
+    float* c_z = comp;
+    float* c_gz = comp + 512;
+    float* sb0 = comp + 1024;
+    float* sb1 = comp + 1536;
+    float* c_P = comp + 2048;
+    float* c_ray = comp + 2176;               // [128 rays][4]: dacc0..2 of each ray
+    const int ntile = a.rpw * S;              // samples of whole rays in this tile
+    const int ls = tid < kTileSamples ? tid : kTileSamples;   // threads >= 128 only sync
+    const int rl = ls / S, j = ls - rl * S;   // ray within the tile, sample within the ray
+    const int ray = wg * a.rpw + rl;
+    const bool valid = ls < ntile && ray < a.rays;
+    const size_t gs = (size_t)ray * S + j;
+    float z[4] = {0, 0, 0, 0}, rgb[3] = {0, 0, 0}, sigma = 0, delta = 0, al = 0, cc = 1;
+    if (valid) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) z[k] = c_z[ls * 4 + k];
+        // head activation (nerf.py:153-167): channel 3 ReLU, 0..2 sigmoid
+#pragma unroll
+        for (int k = 0; k < 3; ++k) rgb[k] = 1.0f / (1.0f + expf(0.0f - z[k]));
+        sigma = (z[3] > 0.0f) ? z[3] : 0.0f;
+        delta = a.dists ? a.dists[gs] : ray_delta(j, S, a.near_t, a.far_t);
+        al = 1.0f - expf((0.0f - sigma) * delta);
+        cc = (1.0f - al) + (float)(1e-10);
+    }
+    // P_j (inclusive product), T_j, w_j
+    float v[4] = {cc, 0, 0, 0};
+    seg_scan_fwd(sb0, sb1, ls, j, S, 1, v, true);
+    const float P = v[0];
+    const float T = (j == 0) ? 1.0f : P;
+    const float w = al * T;
+    if (ls < kTileSamples) c_P[ls] = P;
+    // colour: segmented sum of w * rgb (read at the ray's last sample)
+    float cv[4] = {w * rgb[0], w * rgb[1], w * rgb[2], 0};
+    seg_scan_fwd(sb0, sb1, ls, j, S, 3, cv, false);
+    float loss = 0.0f;
+    const bool last = valid && j == S - 1;
+    if (last) {
+        const float* t = a.target + (size_t)ray * 3;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            loss = loss + (cv[k] - t[k]) * (cv[k] - t[k]);
+            if (a.acc_color) a.acc_color[(size_t)ray * 3 + k] = cv[k];
+        }
+        if (grad) {
+            // reverse of the loss (lg_composite_bwd_kernel): dacc = 2 seed (C - t)
+            for (int k = 2; k >= 0; --k) {
+                const float a1 = (cv[k] - t[k]) * a.seed;
+                const float a2 = 0.0f - ((cv[k] - t[k]) * a.seed);
+                c_ray[rl * 4 + k] = 0.0f + a1 + a1;
+                if (a.d_target) a.d_target[(size_t)ray * 3 + k] = (0.0f + a2) + a2;
+            }
+        }
+    }
+    if (tid < a.rpw) rayloss[tid] = 0.0f;
+    __syncthreads();
+    if (last) rayloss[rl] = loss;
+    if (!grad) return 0.0f;
+
+    // ---- reverse, per sample ----
+    float dacc[3] = {0, 0, 0}, dw = 0.0f, drgb[4] = {0, 0, 0, 0};
+    if (valid) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) dacc[k] = c_ray[rl * 4 + k];
+        for (int k = 2; k >= 0; --k) {
+            dw += rgb[k] * dacc[k];
+            drgb[k] += w * dacc[k];
+        }
+    }
+    float dal = T * dw;
+    // G_j = a_j + c_{j+1} G_{j+1}: segmented suffix scan of (a, b) pairs
+    float ga = (j >= 1) ? al * dw : 0.0f;
+    float gb = 0.0f;
+    if (ls < kTileSamples) sb0[ls] = cc;
+    __syncthreads();
+    if (valid && j + 1 < S) gb = sb0[ls + 1];
+    __syncthreads();
+    {
+        float* cur = sb0;
+        float* nxt = sb1;
+        for (int d = 1; d < S; d <<= 1) {
+            if (ls < kTileSamples) {
+                cur[ls] = ga;
+                cur[kTileSamples + ls] = gb;
+            }
+            __syncthreads();
+            if (ls < kTileSamples && j + d < S) {
+                const float oa = cur[ls + d], ob = cur[kTileSamples + ls + d];
+                ga = ga + gb * oa;
+                gb = gb * ob;
+            }
+            float* t = cur;
+            cur = nxt;
+            nxt = t;
+        }
+    }
+    if (valid) {
+        const float dc = (j >= 1) ? c_P[ls - 1] * ga : ga;
+        dal += 0.0f - dc;                                       // cC = (1 - al) + 1e-10
+        const float adj2 = (0.0f - dal) * expf((0.0f - sigma) * delta);   // alpha reverse
+        drgb[3] += 0.0f - (delta * adj2);
+        if (a.d_dists) a.d_dists[gs] = 0.0f + (0.0f - sigma) * adj2;
+        // head activation reverse (reverse_diff.py Div/exp/Sub rules; ReLU on the post value)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float dz = drgb[k];
+            float g;
+            if (k == 3) {
+                g = (sigma > 0.0f) ? dz : 0.0f;
+            } else {
+                const float x = z[k];
+                const float u = 1.0f + expf(0.0f - x);
+                const float adj_div = ((0.0f - dz) * 1.0f) / (u * u);
+                g = 0.0f + (0.0f - adj_div * expf(0.0f - x));
+            }
+            c_gz[ls * 4 + k] = g;
+        }
+    } else if (ls < kTileSamples) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) c_gz[ls * 4 + k] = 0.0f;
+    }
+    return 0.0f;
+}
+
+}  // namespace comp
+}  // namespace lnerf

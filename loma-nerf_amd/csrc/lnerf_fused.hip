@@ -16,6 +16,7 @@
 //      slabs via LDS, fp32 MFMA; deterministic per-split partials.
 //  k3  reduce kernels        partials -> dW/db in the reference's padded layout, loss, seed scaling.
 #include "lnerf_internal.h"
+#include "lnerf_composite.h"
 
 #include <math.h>
 #include <stdio.h>
@@ -30,10 +31,13 @@ namespace {
 
 constexpr int kWgThreads = 256;
 constexpr int kWaves = 4;
-constexpr int kTileSamples = 128;          // samples per fused workgroup
+constexpr int kTileSamples = comp::kTileSamples;   // samples per fused workgroup
 constexpr int kNT = 8;                     // max 32-wide feature tiles (256 features)
 constexpr int kChunkMax = 16 * 2 * 256;    // floats per staged weight chunk (r x nt4 x 64 lanes x 4)
-constexpr int kCompFloats = 24;            // per-sample compositing scratch floats in LDS
+constexpr int kCompFloats = comp::kCompFloats;     // per-sample compositing scratch floats in LDS
+using comp::composite_tile;
+using comp::input_feature;
+using comp::sample_coord;
 
 // Feature held by accumulator register r of tile t in lane half h (32x32 C/D layout:
 // row = (r&3) + 8(r>>2) + 4h). Using an accumulator as the next MFMA's B operand makes this the
@@ -827,187 +831,6 @@ __device__ __forceinline__ void layer_mma_n(const FusedArgs& a, bool fwd, int l,
     else layer_mma<8, PREC>(a, fwd, l, nchunks, in, out, ring, tstore, tr, nullptr, nullptr);
 }
 
-// Coordinate c of sample row gs: the given point (POINTS) or o + d t in float64 (RAYS).
-__device__ __forceinline__ double sample_coord(const FusedArgs& a, int gs, int c) {
-    if (a.input_mode == LNERF_INPUT_RAYS) {
-        const int ray = gs / a.S, j = gs - ray * a.S;
-        return ray_point(a.x + (size_t)ray * 6, c, j, a.S, a.near_t, a.far_t);
-    }
-    return (double)a.x[(size_t)gs * 3 + c];
-}
-
-__device__ __forceinline__ float input_feature(const FusedArgs& a, int gs, bool valid, int f) {
-    if (!valid || f >= a.k0) return 0.0f;
-    if (a.input_mode == LNERF_INPUT_ENCODED) return a.x[(size_t)gs * a.k0 + f];
-    // positional_encoding_3d (pos_encoding.py:54-66): block-major, float64 trig, rounded once
-    const int c = f % 3, blk = f / 3;
-    const double xc = sample_coord(a, gs, c);
-    if (blk == 0) return (float)xc;
-    const int fb = blk - 1, freq = fb >> 1;
-    const double arg = ldexp(xc, freq);
-    return (fb & 1) ? (float)cos(arg) : (float)sin(arg);
-}
-
-// ---- rendering (nerf.py:176-302), loss and its reverse for one 128-sample tile ----------------
-// One thread per sample (threads 0..127; a ray = S consecutive samples = one scan segment), the
-// along-ray dependencies as segmented Hillis-Steele scans in LDS (log2 S rounds):
-//   forward  P_j = prod_{i<=j} c_i (inclusive, T_0 = 1, T_j = P_j: nerf.py:226-272),
-//            C = sum_j w_j rgb_j (segmented sum, read at the ray's last sample);
-//   reverse  G_j = a_j + c_{j+1} G_{j+1} (the reverse of the inclusive cumprod,
-//            a_j = alpha_j dL/dw_j for j >= 1), dc_j = P_{j-1} G_j, dc_0 = G_0.
-// Every per-sample expression is loma's (composite rules of lnerf_generic.hip); only the
-// association of the along-ray products and sums differs from loma's sequential loops, at fp32
-// rounding level (the parity tolerance covers it; the generic path keeps the exact order).
-// LDS: comp[0..512) z [128][4] (in), [512..1024) gz [128][4] (out), two [4][128] ping-pong scan
-// buffers at 1024 / 1536, P at 2048, per-ray dacc [128][4] at 2176 (kCompFloats = 24 per sample).
-__device__ __forceinline__ void seg_scan_fwd(float* buf0, float* buf1, int ls, int j, int S, int nv,
-                                             float (&v)[4], bool prod_first) {
-    // inclusive segmented scan of nv values (v[0] by product if prod_first, the rest by sum)
-    float* cur = buf0;
-    float* nxt = buf1;
-    for (int d = 1; d < S; d <<= 1) {
-        if (ls < kTileSamples)
-            for (int q = 0; q < nv; ++q) cur[q * kTileSamples + ls] = v[q];
-        __syncthreads();
-        if (ls < kTileSamples && j >= d) {
-            for (int q = 0; q < nv; ++q) {
-                const float o = cur[q * kTileSamples + ls - d];
-                v[q] = (q == 0 && prod_first) ? o * v[q] : o + v[q];
-            }
-        }
-        float* t = cur;
-        cur = nxt;
-        nxt = t;
-    }
-    __syncthreads();   // the next scan may write the buffer this one read last
-}
-
-__device__ __forceinline__ float composite_tile(const FusedArgs& a, int wg, float* comp, float* rayloss,
-                                                bool grad) {
-    const int tid = threadIdx.x, S = a.S;
-    float* c_z = comp;
-    float* c_gz = comp + 512;
-    float* sb0 = comp + 1024;
-    float* sb1 = comp + 1536;
-    float* c_P = comp + 2048;
-    float* c_ray = comp + 2176;               // [128 rays][4]: dacc0..2 of each ray
-    const int ntile = a.rpw * S;              // samples of whole rays in this tile
-    const int ls = tid < kTileSamples ? tid : kTileSamples;   // threads >= 128 only sync
-    const int rl = ls / S, j = ls - rl * S;   // ray within the tile, sample within the ray
-    const int ray = wg * a.rpw + rl;
-    const bool valid = ls < ntile && ray < a.rays;
-    const size_t gs = (size_t)ray * S + j;
-    float z[4] = {0, 0, 0, 0}, rgb[3] = {0, 0, 0}, sigma = 0, delta = 0, al = 0, cc = 1;
-    if (valid) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) z[k] = c_z[ls * 4 + k];
-        // head activation (nerf.py:153-167): channel 3 ReLU, 0..2 sigmoid
-#pragma unroll
-        for (int k = 0; k < 3; ++k) rgb[k] = 1.0f / (1.0f + expf(0.0f - z[k]));
-        sigma = (z[3] > 0.0f) ? z[3] : 0.0f;
-        delta = a.dists ? a.dists[gs] : ray_delta(j, S, a.near_t, a.far_t);
-        al = 1.0f - expf((0.0f - sigma) * delta);
-        cc = (1.0f - al) + (float)(1e-10);
-    }
-    // P_j (inclusive product), T_j, w_j
-    float v[4] = {cc, 0, 0, 0};
-    seg_scan_fwd(sb0, sb1, ls, j, S, 1, v, true);
-    const float P = v[0];
-    const float T = (j == 0) ? 1.0f : P;
-    const float w = al * T;
-    if (ls < kTileSamples) c_P[ls] = P;
-    // colour: segmented sum of w * rgb (read at the ray's last sample)
-    float cv[4] = {w * rgb[0], w * rgb[1], w * rgb[2], 0};
-    seg_scan_fwd(sb0, sb1, ls, j, S, 3, cv, false);
-    float loss = 0.0f;
-    const bool last = valid && j == S - 1;
-    if (last) {
-        const float* t = a.target + (size_t)ray * 3;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            loss = loss + (cv[k] - t[k]) * (cv[k] - t[k]);
-            if (a.acc_color) a.acc_color[(size_t)ray * 3 + k] = cv[k];
-        }
-        if (grad) {
-            // reverse of the loss (lg_composite_bwd_kernel): dacc = 2 seed (C - t)
-            for (int k = 2; k >= 0; --k) {
-                const float a1 = (cv[k] - t[k]) * a.seed;
-                const float a2 = 0.0f - ((cv[k] - t[k]) * a.seed);
-                c_ray[rl * 4 + k] = 0.0f + a1 + a1;
-                if (a.d_target) a.d_target[(size_t)ray * 3 + k] = (0.0f + a2) + a2;
-            }
-        }
-    }
-    if (tid < a.rpw) rayloss[tid] = 0.0f;
-    __syncthreads();
-    if (last) rayloss[rl] = loss;
-    if (!grad) return 0.0f;
-
-    // ---- reverse, per sample ----
-    float dacc[3] = {0, 0, 0}, dw = 0.0f, drgb[4] = {0, 0, 0, 0};
-    if (valid) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) dacc[k] = c_ray[rl * 4 + k];
-        for (int k = 2; k >= 0; --k) {
-            dw += rgb[k] * dacc[k];
-            drgb[k] += w * dacc[k];
-        }
-    }
-    float dal = T * dw;
-    // G_j = a_j + c_{j+1} G_{j+1}: segmented suffix scan of (a, b) pairs
-    float ga = (j >= 1) ? al * dw : 0.0f;
-    float gb = 0.0f;
-    if (ls < kTileSamples) sb0[ls] = cc;
-    __syncthreads();
-    if (valid && j + 1 < S) gb = sb0[ls + 1];
-    __syncthreads();
-    {
-        float* cur = sb0;
-        float* nxt = sb1;
-        for (int d = 1; d < S; d <<= 1) {
-            if (ls < kTileSamples) {
-                cur[ls] = ga;
-                cur[kTileSamples + ls] = gb;
-            }
-            __syncthreads();
-            if (ls < kTileSamples && j + d < S) {
-                const float oa = cur[ls + d], ob = cur[kTileSamples + ls + d];
-                ga = ga + gb * oa;
-                gb = gb * ob;
-            }
-            float* t = cur;
-            cur = nxt;
-            nxt = t;
-        }
-    }
-    if (valid) {
-        const float dc = (j >= 1) ? c_P[ls - 1] * ga : ga;
-        dal += 0.0f - dc;                                       // cC = (1 - al) + 1e-10
-        const float adj2 = (0.0f - dal) * expf((0.0f - sigma) * delta);   // alpha reverse
-        drgb[3] += 0.0f - (delta * adj2);
-        if (a.d_dists) a.d_dists[gs] = 0.0f + (0.0f - sigma) * adj2;
-        // head activation reverse (reverse_diff.py Div/exp/Sub rules; ReLU on the post value)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float dz = drgb[k];
-            float g;
-            if (k == 3) {
-                g = (sigma > 0.0f) ? dz : 0.0f;
-            } else {
-                const float x = z[k];
-                const float u = 1.0f + expf(0.0f - x);
-                const float adj_div = ((0.0f - dz) * 1.0f) / (u * u);
-                g = 0.0f + (0.0f - adj_div * expf(0.0f - x));
-            }
-            c_gz[ls * 4 + k] = g;
-        }
-    } else if (ls < kTileSamples) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) c_gz[ls * 4 + k] = 0.0f;
-    }
-    return 0.0f;
-}
-
 // HT = output tiles of every hidden layer (widths <= 32*HT); the head has <= 32 outputs.
 // PREC: 3 = bf16x6 split-plane MFMA (fp32-accurate, 2.67x the f32 MFMA rate), 1 = plain bf16
 // (one plane; inference), 0 = exact f32 MFMA.
@@ -1653,6 +1476,10 @@ struct Layout {
     int splits[kMaxLayers], phases[kMaxLayers], mode[kMaxLayers], wg_off[kMaxLayers], dw_grid;
     size_t dwp_off[kMaxLayers], dwp_total, dbp_off[kMaxLayers], dbp_total;
     int num_wg, blocks, rpw;
+    // k16 kernel packing (lnerf_k16.hip): 16-wide output tiles, 32-feature k-steps, 3 planes
+    int ht16, ks16_f[kMaxLayers], ks16_b[kMaxLayers], to16_f[kMaxLayers], to16_b[kMaxLayers];
+    size_t w16f_off[kMaxLayers], w16b_off[kMaxLayers], w16_total;   // u16
+    size_t b16_total;                                                 // floats
 };
 
 inline int pow2_tiles(int t) { return t <= 1 ? 1 : t <= 2 ? 2 : t <= 4 ? 4 : 8; }
@@ -1692,6 +1519,21 @@ void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S, bool train = tr
         y.w6b_off[l] = off; off += align_up(y.w6b_n[l], 512);
     }
     y.w6_total = off;
+    int mx16 = 1;
+    for (int l = 0; l + 1 < L; ++l) mx16 = (m.n[l] + 15) / 16 > mx16 ? (m.n[l] + 15) / 16 : mx16;
+    y.ht16 = mx16 <= 1 ? 1 : mx16 <= 2 ? 2 : mx16 <= 4 ? 4 : mx16 <= 8 ? 8 : 16;
+    const int k0t16 = (m.k[0] + 15) / 16;
+    off = 0;
+    for (int l = 0; l < L; ++l) {
+        y.ks16_f[l] = (m.k[l] + 31) / 32;
+        y.ks16_b[l] = (m.n[l] + 31) / 32;
+        y.to16_f[l] = (l < L - 1) ? y.ht16 : 1;
+        y.to16_b[l] = (l >= 1) ? y.ht16 : (k0t16 <= 1 ? 1 : k0t16 <= 2 ? 2 : k0t16 <= 4 ? 4 : k0t16 <= 8 ? 8 : 16);
+        y.w16f_off[l] = off; off += align_up((size_t)y.ks16_f[l] * y.to16_f[l] * 3 * 512, 512);
+        y.w16b_off[l] = off; off += align_up((size_t)y.ks16_b[l] * y.to16_b[l] * 3 * 512, 512);
+    }
+    y.w16_total = off;
+    y.b16_total = (size_t)L * 256;
     y.rpw = S >= kTileSamples ? 1 : kTileSamples / S;
     y.num_wg = (rays + y.rpw - 1) / y.rpw;
     y.blocks = y.num_wg * kWaves;
@@ -1760,7 +1602,7 @@ size_t fused_workspace_bytes(const lnerf_mlp& m, int rays, int S, bool train) {
     size_t f = align_up(y.pack_total, 64) + align_up((y.w6_total + 1) / 2, 64) +
                align_up(y.act_total, 64) + align_up(y.grad_total, 64) +
                align_up((size_t)y.num_wg, 64) + align_up(y.dwp_total, 64) + align_up(y.dbp_total, 64) +
-               64;
+               64 + align_up((y.w16_total + 1) / 2, 64) + align_up(y.b16_total, 64);
     return f * sizeof(float);
 }
 
@@ -1829,7 +1671,24 @@ void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws
     p.db_part = base + off;
     off += align_up(y.dbp_total, 64);
     p.loss_total = base + off;
+    off += 64;
+    p.w16 = (unsigned short*)(base + off);
+    off += align_up((y.w16_total + 1) / 2, 64);
+    p.b16 = base + off;
+    off += align_up(y.b16_total, 64);
     p.x_off = y.x_off;
+    p.ht16 = y.ht16;
+    for (int l = 0; l < p.L; ++l) {
+        p.ks16_f[l] = y.ks16_f[l];
+        p.ks16_b[l] = y.ks16_b[l];
+        p.to16_f[l] = y.to16_f[l];
+        p.to16_b[l] = y.to16_b[l];
+        p.w16f_off[l] = y.w16f_off[l];
+        p.w16b_off[l] = y.w16b_off[l];
+    }
+    // LNERF_K16=0 selects the one-wave-per-SIMD kernel (fused_fwd_bwd_kernel) for A/B runs
+    const char* e = getenv("LNERF_K16");
+    p.k16 = (e && e[0] == '0') ? 0 : (k16_supported(p) ? 1 : 0);
 }
 
 static void launch_pack(const FusedPlan& p, const float* ws, const float* bs, hipStream_t s) {
@@ -1961,10 +1820,15 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
         if (ev) (void)hipEventRecord(ev[i], s);
     };
     mark(0);
-    launch_pack(p, ws, bs, s);
+    if (p.k16) k16_pack(p, ws, bs, s);
+    else launch_pack(p, ws, bs, s);
     mark(1);
-    FusedArgs fa = make_fused_args(p, b, seed_loss ? 1.0f : seed, out, true);
-    launch_fused(p, fa, s);
+    if (p.k16) {
+        k16_launch(p, b, seed_loss ? 1.0f : seed, out, true, s);
+    } else {
+        FusedArgs fa = make_fused_args(p, b, seed_loss ? 1.0f : seed, out, true);
+        launch_fused(p, fa, s);
+    }
 #if LNERF_PROF
     prof_report(p, s);
 #endif
@@ -2028,9 +1892,14 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
 
 void fused_render(const FusedPlan& p, const float* ws, const float* bs, const lnerf_batch& b,
                   const lnerf_outputs& out, hipStream_t s) {
-    launch_pack(p, ws, bs, s);
-    FusedArgs fa = make_fused_args(p, b, 1.0f, out, false);
-    launch_fused(p, fa, s);
+    if (p.k16) {
+        k16_pack(p, ws, bs, s);
+        k16_launch(p, b, 1.0f, out, false, s);
+    } else {
+        launch_pack(p, ws, bs, s);
+        FusedArgs fa = make_fused_args(p, b, 1.0f, out, false);
+        launch_fused(p, fa, s);
+    }
     loss_reduce_kernel<<<1, 256, 0, s>>>(p.loss_part, p.num_wg, p.loss_total, out.loss);
 }
 

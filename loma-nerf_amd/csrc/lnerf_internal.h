@@ -148,6 +148,14 @@ struct FusedPlan {
     size_t dbp_off[kMaxLayers];
     int dw_grid;
     float* loss_total; // device scalar
+    // k16 kernel (lnerf_k16.hip): 512-thread workgroups, two waves per SIMD, 16x16x32 MFMA
+    int k16;                             // 1: the fused step runs k16 (pack16 + k16 kernel)
+    int ht16;                            // 16-wide hidden output tiles (1/2/4/8/16)
+    int ks16_f[kMaxLayers], ks16_b[kMaxLayers];   // k-steps (32 features) per pass
+    int to16_f[kMaxLayers], to16_b[kMaxLayers];   // 16-wide output tiles per pass
+    unsigned short* w16;                 // packed planes, u16 offsets below
+    size_t w16f_off[kMaxLayers], w16b_off[kMaxLayers];
+    float* b16;                          // [L][256] zero-padded biases
 };
 
 bool fused_supported(const lnerf_mlp& mlp, int rays, int S, int input_mode, const char** why);
@@ -162,5 +170,10 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
                       hipEvent_t* ev);
 void fused_render(const FusedPlan& p, const float* ws, const float* bs, const lnerf_batch& b,
                   const lnerf_outputs& out, hipStream_t s);
+// k16 kernel entry points (lnerf_k16.hip)
+bool k16_supported(const FusedPlan& p);
+void k16_pack(const FusedPlan& p, const float* ws, const float* bs, hipStream_t s);
+void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lnerf_outputs& out,
+                bool want_grad, hipStream_t s);
 
 }  // namespace lnerf

@@ -1,0 +1,549 @@
+// lnerf_k16.hip -- k1 on wave pairs: the fused PE + MLP + compositing + reverse chain with two
+// waves per SIMD (v_mfma_f32_16x16x32_bf16), the default fused kernel for the bf16 precisions.
+//
+// Same work and outputs as fused_fwd_bwd_kernel (lnerf_fused.hip; reference scripts/nerf.py:1-304
+// and its rev_diff, train_nerf.py:325/395), re-tiled so that a CU holds TWO waves per SIMD:
+//  * one 512-thread workgroup (8 waves) per 128-sample tile of whole rays; each wave owns 16
+//    samples, so a 256-wide layer is 16 accumulator tiles x 4 registers = 64 registers for the
+//    activations and 64 for the accumulators, and the kernel fits 256 registers per lane;
+//  * the activations stay in the transposed accumulator layout (lane = sample l & 15, registers
+//    = features 4(l >> 4) + i of each 16-feature tile), which is the next layer's B operand after
+//    a fixed permutation of the contraction order (phi below) baked into the weight packing;
+//  * the weights of one k-step (32 input features x every output tile, in the 3 bf16 planes of
+//    the bf16x6 split) stream through a 2-slot LDS ring by LDS-DMA, one barrier per k-step;
+//  * while one wave of a SIMD issues its LDS reads, operand splits, slab stores, DMA pieces or
+//    epilogue, its partner's MFMAs keep the matrix core busy -- the latency hiding that the
+//    one-wave-per-SIMD kernel had to hand-schedule.
+// The slabs (post-ReLU activations A_l, gradients G_l) are written in the layout the dW kernel
+// reads (lnerf_fused.hip slab_off): a wave owns one 16-sample half of a 32-sample block.
+#include "lnerf_composite.h"
+#include "lnerf_internal.h"
+
+namespace lnerf {
+
+namespace {
+
+typedef float fx4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+
+constexpr int kThreads = 512;
+constexpr int kWaves = 8;
+constexpr int kTile = comp::kTileSamples;     // 128 samples per workgroup
+constexpr int kMaxT = 16;                     // 16-feature tiles per 256-wide layer
+constexpr int kSlotBytes = kMaxT * 3 * 1024;  // one k-step of a 256-output layer, 3 planes
+constexpr int kMaxMaskLayers = 8;
+constexpr int kOffMask = 2 * kSlotBytes;
+constexpr int kOffComp = kOffMask + kMaxMaskLayers * kWaves * 64 * 8;
+constexpr int kOffRay = kOffComp + kTile * comp::kCompFloats * 4;
+constexpr int kOffBias = kOffRay + kTile * 4;
+constexpr int kLdsBytes = kOffBias + 2 * 256 * 4;
+static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
+
+struct K16Args {
+    int L;
+    int ks_f[kMaxLayers], ks_b[kMaxLayers];   // k-steps (32 input features) per pass
+    int to_f[kMaxLayers], to_b[kMaxLayers];   // 16-wide output tiles per pass
+    int kt[kMaxLayers], nt[kMaxLayers];       // 32-wide slab tiles of each layer's input/output
+    int k0;
+    const unsigned short* w16;
+    size_t wf_off[kMaxLayers], wb_off[kMaxLayers];   // u16 offsets
+    const float* b16;                                // [L][256] zero-padded biases
+    float* act;
+    size_t act_off[kMaxLayers];
+    size_t x_off;
+    float* grad;
+    size_t grad_off[kMaxLayers];
+    int rays, S, rpw, R, input_mode, F;
+    float near_t, far_t;
+    const float* x;
+    const float* dists;
+    const float* target;
+    float* loss_part;
+    float* acc_color;
+    float* d_dists;
+    float* d_target;
+    float* d_x;
+    float seed;
+    int want_grad;
+    int planes;
+};
+
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+// Input feature of k-step s held in element j of a lane in lane group g (the B operand's
+// k = 8g + j): tile 2s + (j >> 2), register j & 3 of that lane.
+__host__ __device__ __forceinline__ int phi(int s, int g, int j) {
+    return 32 * s + 16 * (j >> 2) + 4 * g + (j & 3);
+}
+
+// One chunk of packed weights (one k-step of one pass) and, for the first chunk of a forward
+// pass, the layer's biases.
+struct Chunk {
+    const unsigned short* src;
+    int bytes;
+    const float* bias;
+    int bias_slot;
+};
+
+__device__ __forceinline__ Chunk pass_chunk(const K16Args& a, bool fwd, int l, int s) {
+    const int to = fwd ? a.to_f[l] : a.to_b[l];
+    const size_t per = (size_t)to * a.planes * 512;   // u16 per chunk
+    Chunk c;
+    c.src = a.w16 + (fwd ? a.wf_off[l] : a.wb_off[l]) + (size_t)s * per;
+    c.bytes = (int)(per * 2);
+    c.bias = (fwd && s == 0) ? a.b16 + (size_t)l * 256 : nullptr;
+    c.bias_slot = l & 1;
+    return c;
+}
+
+__device__ __forceinline__ Chunk no_chunk() { return Chunk{nullptr, 0, nullptr, 0}; }
+
+// The first chunk of the pass that follows pass (fwd, l) in the kernel's order: forward 0..L-1,
+// then (training) backward L-1..1, and backward 0 when d_x is wanted.
+__device__ __forceinline__ Chunk next_pass_chunk(const K16Args& a, bool fwd, int l) {
+    int nl;
+    bool nf;
+    if (fwd) {
+        if (l + 1 < a.L) return pass_chunk(a, true, l + 1, 0);
+        if (!a.want_grad) return no_chunk();
+        nf = false;
+        nl = a.L - 1;
+    } else {
+        nf = false;
+        nl = l - 1;
+    }
+    if (nl < 0 || (nl == 0 && !a.d_x)) return no_chunk();
+    return pass_chunk(a, nf, nl, 0);
+}
+
+// LDS-DMA (global_load_lds_dwordx4) of `bytes` (a multiple of 1 KiB) into `dst`: 8 KiB per
+// round of the workgroup, each wave instruction 1 KiB (lane-linear).
+__device__ __forceinline__ void dma_chunk(const Chunk& c, unsigned char* dst, float* bias_lds) {
+    const int tid = threadIdx.x, wave = wave_id();
+    for (int off = wave * 1024; off < c.bytes; off += kThreads * 16) {
+        const char* g = (const char*)c.src + off + (tid & 63) * 16;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                         (__attribute__((address_space(3))) void*)(dst + off), 16, 0, 0);
+    }
+    if (c.bias && wave == kWaves - 1) {
+        const float* g = c.bias + (tid & 63) * 4;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                         (__attribute__((address_space(3))) void*)(bias_lds + c.bias_slot * 256),
+                                         16, 0, 0);
+    }
+}
+
+// Every wave's LDS-DMA has landed and every wave is done with the slot it read:
+// vmcnt(0) (loads and stores share the counter) + s_barrier.
+__device__ __forceinline__ void dma_barrier() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), expcnt(7), lgkmcnt(15)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ fx4 mfma16(const bf8& a, const bf8& b, fx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// x = hi + mid + lo (round-to-nearest bf16 of each remainder; every remainder is exact in f32)
+__device__ __forceinline__ void split_x(float x, __bf16& h, __bf16& m, __bf16& l) {
+    h = (__bf16)x;
+    const float r = x - (float)h;
+    m = (__bf16)r;
+    l = (__bf16)(r - (float)m);
+}
+
+// Slab tile store: the 8 features of k-step s that a lane holds (rows phi - 32 s of the
+// 32-feature tile) for its sample n, into [32 rows][16 samples] of this wave's half. Each wave
+// instruction writes 4 runs of 64 B.
+__device__ __forceinline__ void store_slab_step(float* __restrict__ dst, const fx4& t0, const fx4& t1) {
+    const int lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int row = 16 * (j >> 2) + 4 * g + (j & 3);
+        __builtin_nontemporal_store(j < 4 ? t0[j] : t1[j - 4], dst + row * 16 + n);
+    }
+}
+
+// One pass (a layer's forward or backward MMA): out[o] += sum over the pass's k-steps of
+// Wpack[s][o] (x) in[2s..2s+1], NTO output tiles, chunk s streamed through the ring while chunk
+// s + 1 (or the next pass's first chunk) is in flight. `slab` (nullable) receives the input
+// tiles (the A_{l-1} or G_l slab of this wave's half-block).
+template <int NTO, int PL>
+__device__ __forceinline__ void k16_pass(const K16Args& a, Chunk cur, int ks, Chunk nxt, int& slot,
+                                         unsigned char* ring, float* bias_lds, const fx4 (&in)[kMaxT],
+                                         fx4 (&out)[kMaxT], float* __restrict__ slab) {
+    const int lane = threadIdx.x & 63;
+    const size_t per = (size_t)NTO * PL * 512;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        if (s < ks) {
+            const unsigned char* buf = ring + slot * kSlotBytes;
+            Chunk n = nxt;
+            if (s + 1 < ks) {
+                n = cur;
+                n.src = cur.src + (size_t)(s + 1) * per;
+                n.bias = nullptr;
+            }
+            if (n.src) dma_chunk(n, ring + (slot ^ 1) * kSlotBytes, bias_lds);
+            if (slab) store_slab_step(slab + s * 1024, in[2 * s], in[2 * s + 1]);
+            bf8 bh, bm, bl;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float x = j < 4 ? in[2 * s][j] : in[2 * s + 1][j - 4];
+                if (PL == 3) {
+                    __bf16 h, m, l;
+                    split_x(x, h, m, l);
+                    bh[j] = h;
+                    bm[j] = m;
+                    bl[j] = l;
+                } else {
+                    bh[j] = (__bf16)x;
+                }
+            }
+            const bf8* wp = (const bf8*)(buf + lane * 16);
+#pragma unroll
+            for (int o = 0; o < NTO; ++o) {
+                if (PL == 3) {
+                    const bf8 wh = wp[(o * 3 + 0) * 64], wm = wp[(o * 3 + 1) * 64], wl = wp[(o * 3 + 2) * 64];
+                    fx4 acc = out[o];
+                    acc = mfma16(wh, bl, acc);   // small terms first
+                    acc = mfma16(wm, bm, acc);
+                    acc = mfma16(wl, bh, acc);
+                    acc = mfma16(wm, bh, acc);
+                    acc = mfma16(wh, bm, acc);
+                    acc = mfma16(wh, bh, acc);
+                    out[o] = acc;
+                } else {
+                    out[o] = mfma16(wp[o * 64], bh, out[o]);
+                }
+            }
+            dma_barrier();
+            slot ^= 1;
+        }
+    }
+    (void)cur;
+}
+
+template <int PL>
+__device__ __forceinline__ void k16_pass_n(const K16Args& a, Chunk cur, int ks, Chunk nxt, int& slot,
+                                           unsigned char* ring, float* bias_lds, int nto,
+                                           const fx4 (&in)[kMaxT], fx4 (&out)[kMaxT], float* slab) {
+    if (nto <= 1) k16_pass<1, PL>(a, cur, ks, nxt, slot, ring, bias_lds, in, out, slab);
+    else if (nto <= 2) k16_pass<2, PL>(a, cur, ks, nxt, slot, ring, bias_lds, in, out, slab);
+    else if (nto <= 4) k16_pass<4, PL>(a, cur, ks, nxt, slot, ring, bias_lds, in, out, slab);
+    else if (nto <= 8) k16_pass<8, PL>(a, cur, ks, nxt, slot, ring, bias_lds, in, out, slab);
+    else k16_pass<16, PL>(a, cur, ks, nxt, slot, ring, bias_lds, in, out, slab);
+}
+
+__device__ __forceinline__ void zero_tiles(fx4 (&t)[kMaxT]) {
+#pragma unroll
+    for (int o = 0; o < kMaxT; ++o) t[o] = fx4{0.0f, 0.0f, 0.0f, 0.0f};
+}
+
+// HT: 16-wide output tiles of every hidden layer (1/2/4/8/16); PL: bf16 planes (3 = bf16x6,
+// fp32-accurate; 1 = plain bf16, inference).
+template <int HT, int PL>
+__global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
+    __shared__ __attribute__((aligned(16))) unsigned char lds[kLdsBytes];
+    unsigned char* ring = lds;
+    unsigned long long* masks = (unsigned long long*)(lds + kOffMask);
+    float* comp = (float*)(lds + kOffComp);
+    float* rayloss = (float*)(lds + kOffRay);
+    float* bias_lds = (float*)(lds + kOffBias);
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id(), g = lane >> 4, n = lane & 15;
+    const int wg = blockIdx.x;
+    const int tile_samples = a.rpw * a.S;
+    const int ls = wave * 16 + n;                      // local sample 0..127
+    const int gs = wg * tile_samples + ls;             // global sample row (ray*S + j)
+    const bool valid = (ls < tile_samples) && (gs < a.R);
+    const size_t blk = (size_t)wg * 4 + (wave >> 1);   // 32-sample slab block
+    const int half = wave & 1;
+    const bool st = a.want_grad != 0;
+
+    fx4 act[kMaxT], out[kMaxT];
+    zero_tiles(act);
+
+    // ---- layer-0 input in the accumulator layout, through a per-wave LDS scratch (the ring is
+    // free before the first DMA). POINTS/RAYS with k0 <= 64: one float64 sincos per (sample,
+    // coordinate, frequency) (pos_encoding.py:54-66); otherwise tile by tile.
+    const int tile_base = wg * tile_samples + wave * 16;
+    if (a.input_mode != LNERF_INPUT_ENCODED && a.k0 <= 64) {
+        constexpr int kStride = 65;
+        float* pe = (float*)ring + wave * (16 * kStride);
+        const int F = a.F, per = 3 * (F + 1);
+        for (int it = lane; it < 16 * per; it += 64) {
+            const int sl = it / per, rem = it - sl * per, c = rem % 3, q = rem / 3;
+            const bool vs = (wave * 16 + sl < tile_samples) && (tile_base + sl < a.R);
+            const double xc = vs ? comp::sample_coord(a, tile_base + sl, c) : 0.0;
+            if (q == 0) {
+                pe[sl * kStride + c] = (float)xc;
+            } else {
+                double sn, cs;
+                sincos(ldexp(xc, q - 1), &sn, &cs);
+                pe[sl * kStride + 3 + 6 * (q - 1) + c] = (float)sn;
+                pe[sl * kStride + 6 + 6 * (q - 1) + c] = (float)cs;
+            }
+        }
+        for (int e = lane; e < 16 * 64; e += 64) {
+            const int sl = e >> 6, f = e & 63;
+            if (f >= a.k0) pe[sl * kStride + f] = 0.0f;
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) act[t][i] = pe[n * kStride + 16 * t + 4 * g + i];
+    } else {
+        float* pe = (float*)ring + wave * (16 * 17);
+#pragma unroll
+        for (int t = 0; t < kMaxT; ++t) {
+            if (16 * t < a.k0) {
+                for (int e = lane; e < 256; e += 64) {
+                    const int sl = e >> 4, ft = e & 15;
+                    const bool vs = (wave * 16 + sl < tile_samples) && (tile_base + sl < a.R);
+                    pe[sl * 17 + ft] = comp::input_feature(a, tile_base + sl, vs, 16 * t + ft);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) act[t][i] = pe[n * 17 + 4 * g + i];
+            }
+        }
+    }
+    __syncthreads();   // the first DMA overwrites the scratch
+
+    int slot = 0;
+    {
+        const Chunk c0 = pass_chunk(a, true, 0, 0);
+        dma_chunk(c0, ring, bias_lds);
+        dma_barrier();
+    }
+
+    // ---- forward ----
+    for (int l = 0; l < a.L; ++l) {
+        zero_tiles(out);
+        float* slab = !st ? nullptr
+                          : (l == 0 ? a.act + a.x_off + blk * (size_t)(a.kt[0] * 1024)
+                                    : a.act + a.act_off[l - 1] + blk * (size_t)(a.kt[l] * 1024)) +
+                                half * 512;
+        const Chunk c = pass_chunk(a, true, l, 0);
+        const Chunk nx = next_pass_chunk(a, true, l);
+        const float* bl = bias_lds + (l & 1) * 256;
+        if (l < a.L - 1) {
+            k16_pass<HT, PL>(a, c, a.ks_f[l], nx, slot, ring, bias_lds, act, out, slab);
+            // bias after the sum (nerf.py:98,125), ReLU (nerf.py:141-144), mask bits
+            unsigned long long mb = 0ull;
+#pragma unroll
+            for (int o = 0; o < HT; ++o) {
+                const fx4 b4 = *(const fx4*)(bl + 16 * o + 4 * g);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float v = out[o][i] + b4[i];
+                    const bool pos = v > 0.0f;
+                    act[o][i] = pos ? v : 0.0f;
+                    mb |= (pos ? 1ull : 0ull) << (4 * o + i);
+                }
+            }
+            masks[((size_t)l * kWaves + wave) * 64 + lane] = mb;
+        } else {
+            k16_pass<1, PL>(a, c, a.ks_f[l], nx, slot, ring, bias_lds, act, out, slab);
+            // head pre-activations: features 0..3 = registers 0..3 of lane group 0
+            if (g == 0) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) comp[ls * 4 + i] = out[0][i] + bl[i];
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- rendering + loss + rendering reverse (one thread per sample, scans along rays) ----
+    comp::composite_tile(a, wg, comp, rayloss, st);
+    __syncthreads();
+    if (tid == 0) {
+        float lsum = 0.0f;
+        for (int r = 0; r < a.rpw; ++r) lsum = lsum + rayloss[r];
+        a.loss_part[wg] = lsum;
+    }
+    if (!st) return;
+
+    // ---- reverse chain: G_{L-1} from the head, G_{l-1} = (W_l G_l) * 1[A_{l-1} > 0] ----
+    const float* c_gz = comp + 512;
+    zero_tiles(act);
+    if (g == 0 && valid) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) act[0][i] = c_gz[ls * 4 + i];
+    }
+    for (int l = a.L - 1; l >= 1; --l) {
+        zero_tiles(out);
+        float* slab = a.grad + a.grad_off[l] + blk * (size_t)(a.nt[l] * 1024) + half * 512;
+        k16_pass<HT, PL>(a, pass_chunk(a, false, l, 0), a.ks_b[l], next_pass_chunk(a, false, l), slot,
+                         ring, bias_lds, act, out, slab);
+        const unsigned long long mb = masks[((size_t)(l - 1) * kWaves + wave) * 64 + lane];
+#pragma unroll
+        for (int o = 0; o < HT; ++o)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) act[o][i] = ((mb >> (4 * o + i)) & 1ull) ? out[o][i] : 0.0f;
+    }
+    // act holds G_0
+    float* g0 = a.grad + a.grad_off[0] + blk * (size_t)(a.nt[0] * 1024) + half * 512;
+    if (a.d_x) {
+        // d_layer_input = G_0 W_0^T (ENCODED mode); the pass also writes G_0's slab
+        zero_tiles(out);
+        k16_pass_n<PL>(a, pass_chunk(a, false, 0, 0), a.ks_b[0], no_chunk(), slot, ring, bias_lds,
+                       a.to_b[0], act, out, g0);
+        if (valid) {
+#pragma unroll
+            for (int o = 0; o < kMaxT; ++o)
+                if (16 * o < a.k0) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int f = 16 * o + 4 * g + i;
+                        if (f < a.k0) a.d_x[(size_t)gs * a.k0 + f] = out[o][i];
+                    }
+                }
+        }
+    } else {
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+            if (s < a.ks_b[0]) store_slab_step(g0 + s * 1024, act[2 * s], act[2 * s + 1]);
+    }
+}
+
+// ---- weight packing: per layer and pass, chunk s = [o][plane][lane 64][8 x bf16] -----------
+// forward:  A[m = out 16o + (lane & 15)][k = 8g + j] = W[phi(s, g, j)][16o + m]
+// backward: A[m = in  16o + (lane & 15)][k = 8g + j] = W[16o + m][phi(s, g, j)]
+struct Pack16Args {
+    int L;
+    int k[kMaxLayers], n[kMaxLayers];
+    int ks_f[kMaxLayers], ks_b[kMaxLayers], to_f[kMaxLayers], to_b[kMaxLayers];
+    int w_k, w_n, planes;
+    const float* W;
+    const float* B;
+    unsigned short* w16;
+    size_t wf_off[kMaxLayers], wb_off[kMaxLayers];
+    float* b16;
+};
+
+__global__ void pack16_kernel(Pack16Args a, int l) {
+    const float* W = a.W + (size_t)l * a.w_k * a.w_n;
+    const int K = a.k[l], N = a.n[l];
+    const size_t nf = (size_t)a.ks_f[l] * a.to_f[l] * 512, nb = (size_t)a.ks_b[l] * a.to_b[l] * 512;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < nf + nb + 256;
+         e += (size_t)gridDim.x * blockDim.x) {
+        if (e >= nf + nb) {
+            const int f = (int)(e - nf - nb);
+            a.b16[(size_t)l * 256 + f] = f < N ? a.B[(size_t)l * a.w_n + f] : 0.0f;
+            continue;
+        }
+        const bool fwd = e < nf;
+        size_t x = fwd ? e : e - nf;
+        const int to = fwd ? a.to_f[l] : a.to_b[l];
+        const int j = x & 7; x >>= 3;
+        const int ln = x & 63; x >>= 6;
+        const int o = (int)(x % to); x /= to;
+        const int s = (int)x;
+        const int f = phi(s, ln >> 4, j), m = 16 * o + (ln & 15);
+        const int kk = fwd ? f : m, jj = fwd ? m : f;
+        const float w = (kk < K && jj < N) ? W[(size_t)kk * a.w_n + jj] : 0.0f;
+        __bf16 h, mi, lo;
+        split_x(w, h, mi, lo);
+        unsigned short* dst = a.w16 + (fwd ? a.wf_off[l] : a.wb_off[l]) +
+                              ((size_t)(s * to + o) * a.planes) * 512 + ln * 8 + j;
+        dst[0] = __builtin_bit_cast(unsigned short, h);
+        if (a.planes == 3) {
+            dst[512] = __builtin_bit_cast(unsigned short, mi);
+            dst[1024] = __builtin_bit_cast(unsigned short, lo);
+        }
+    }
+}
+
+}  // namespace
+
+bool k16_supported(const FusedPlan& p) {
+    if (p.x6 != 3 && p.x6 != 1) return false;
+    if (p.L - 1 > kMaxMaskLayers) return false;
+    if (p.n[p.L - 1] > 16) return false;       // head: one 16-wide output tile
+    return true;
+}
+
+void k16_pack(const FusedPlan& p, const float* ws, const float* bs, hipStream_t s) {
+    Pack16Args a{};
+    a.L = p.L;
+    for (int l = 0; l < p.L; ++l) {
+        a.k[l] = p.k[l];
+        a.n[l] = p.n[l];
+        a.ks_f[l] = p.ks16_f[l];
+        a.ks_b[l] = p.ks16_b[l];
+        a.to_f[l] = p.to16_f[l];
+        a.to_b[l] = p.to16_b[l];
+        a.wf_off[l] = p.w16f_off[l];
+        a.wb_off[l] = p.w16b_off[l];
+    }
+    a.w_k = p.w_k;
+    a.w_n = p.w_n;
+    a.planes = p.x6;
+    a.W = ws;
+    a.B = bs;
+    a.w16 = p.w16;
+    a.b16 = p.b16;
+    for (int l = 0; l < p.L; ++l) {
+        const size_t nel = ((size_t)a.ks_f[l] * a.to_f[l] + (size_t)a.ks_b[l] * a.to_b[l]) * 512 + 256;
+        pack16_kernel<<<(unsigned)((nel + 255) / 256), 256, 0, s>>>(a, l);
+    }
+}
+
+void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lnerf_outputs& out,
+                bool want_grad, hipStream_t s) {
+    K16Args a{};
+    a.L = p.L;
+    for (int l = 0; l < p.L; ++l) {
+        a.ks_f[l] = p.ks16_f[l];
+        a.ks_b[l] = p.ks16_b[l];
+        a.to_f[l] = p.to16_f[l];
+        a.to_b[l] = p.to16_b[l];
+        a.kt[l] = p.kt[l];
+        a.nt[l] = p.nt[l];
+        a.wf_off[l] = p.w16f_off[l];
+        a.wb_off[l] = p.w16b_off[l];
+        a.act_off[l] = p.act_off[l];
+        a.grad_off[l] = p.grad_off[l];
+    }
+    a.k0 = p.k[0];
+    a.w16 = p.w16;
+    a.b16 = p.b16;
+    a.act = p.act;
+    a.x_off = p.x_off;
+    a.grad = p.grad;
+    a.rays = p.rays;
+    a.S = p.S;
+    a.rpw = p.rays_per_wg;
+    a.R = p.R;
+    a.input_mode = b.input_mode;
+    a.F = b.num_freqs;
+    a.near_t = b.near_t;
+    a.far_t = b.far_t;
+    a.x = b.x;
+    a.dists = b.input_mode == LNERF_INPUT_RAYS ? nullptr : b.dists;
+    a.target = b.target;
+    a.loss_part = p.loss_part;
+    a.acc_color = out.acc_color;
+    a.d_dists = want_grad ? out.d_dists : nullptr;
+    a.d_target = want_grad ? out.d_target : nullptr;
+    a.d_x = want_grad ? out.d_x : nullptr;
+    a.seed = seed;
+    a.want_grad = want_grad ? 1 : 0;
+    a.planes = p.x6;
+#define LNERF_K16_LAUNCH(HT)                                                              \
+    if (p.x6 == 3) k16_fwd_bwd_kernel<HT, 3><<<p.num_wg, kThreads, 0, s>>>(a);            \
+    else k16_fwd_bwd_kernel<HT, 1><<<p.num_wg, kThreads, 0, s>>>(a);
+    switch (p.ht16) {
+        case 1: LNERF_K16_LAUNCH(1) break;
+        case 2: LNERF_K16_LAUNCH(2) break;
+        case 4: LNERF_K16_LAUNCH(4) break;
+        case 8: LNERF_K16_LAUNCH(8) break;
+        default: LNERF_K16_LAUNCH(16) break;
+    }
+#undef LNERF_K16_LAUNCH
+}
+
+}  // namespace lnerf

@@ -157,6 +157,38 @@ def make_workload(name: str = "cfg2", rays: int | None = None, samples: int | No
     return Workload(pts, pts32, X, dists.astype(np.float32), target, ws, bs, wp, bp, F, S, N)
 
 
+def relu_tie_rays(w: Workload, thresh: float = 5e-7) -> np.ndarray:
+    """Rays holding a hidden pre-activation z with |z| < thresh * sum|terms| (float64 forward).
+
+    Such a ReLU decision sits below fp32 resolution (thresh ~ 8 ulp): any fp32 summation order
+    may decide it either way, and a flipped decision moves that sample's whole gradient row, far
+    past the 1e-4 parity tolerance ("ReLU-mask flips ... reported separately")."""
+    A = positional_encoding_3d(w.pts32.astype(np.float64), w.F).reshape(w.N * w.S, -1) \
+        if w.X.shape[1] == 3 + 6 * w.F else w.X.astype(np.float64)
+    bad = np.zeros(w.N * w.S, bool)
+    for l in range(len(w.ws) - 1):
+        W = w.ws[l].astype(np.float64)
+        b = w.bs[l].astype(np.float64)
+        Z = A @ W + b
+        T = np.abs(A) @ np.abs(W) + np.abs(b)
+        bad |= (np.abs(Z) < thresh * T).any(axis=1)
+        A = np.maximum(Z, 0.0)
+    return np.unique(np.nonzero(bad)[0] // w.S)
+
+
+def subset_rays(w: Workload, rays) -> Workload:
+    rays = np.asarray(rays, np.int64)
+    rows = (rays[:, None] * w.S + np.arange(w.S)[None, :]).ravel()
+    return Workload(w.pts[rays], w.pts32[rays], w.X[rows], w.dists[rays], w.target[rays], w.ws, w.bs,
+                    w.wp, w.bp, w.F, w.S, len(rays))
+
+
+def without_relu_ties(w: Workload, thresh: float = 5e-7) -> Workload:
+    """The workload minus its relu_tie_rays (parity tests against an fp32 oracle)."""
+    ties = set(relu_tie_rays(w, thresh).tolist())
+    return subset_rays(w, [r for r in range(w.N) if r not in ties])
+
+
 # --------------------------------------------------------------------------------------------
 # float64 forward + hand-derived backward (standard semantics)
 # --------------------------------------------------------------------------------------------

@@ -19,6 +19,8 @@
 #include "lnerf_composite.h"
 #include "lnerf_internal.h"
 
+#include <utility>
+
 namespace lnerf {
 
 namespace {
@@ -166,6 +168,68 @@ __device__ __forceinline__ void store_slab_step(float* __restrict__ dst, const f
     }
 }
 
+// LDS byte address of a pointer into __shared__ memory.
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+    return (unsigned)(size_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// ds_read_b128 with an immediate offset, outside the compiler's waitcnt bookkeeping: the
+// matching lgkm_wait below is the only wait, so reads of later tiles stay in flight.
+template <int OFF>
+__device__ __forceinline__ bf8 ds_read_at(unsigned addr) {
+    bf8 r;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+    return r;
+}
+
+// s_waitcnt lgkmcnt(N) that the fragments depend on (no use can be scheduled above it). LDS
+// reads return in order, so at most N outstanding means every older read has landed.
+template <int N>
+__device__ __forceinline__ void lgkm_wait(bf8 (&w)[3]) {
+    asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]) : "n"(N));
+}
+
+constexpr int kDist = 2;   // weight tiles read ahead of the one the MFMAs consume
+
+template <int PL, int O>
+__device__ __forceinline__ void read_tile(unsigned base, bf8 (&w)[3]) {
+    w[0] = ds_read_at<(O * PL + 0) * 1024>(base);
+    if constexpr (PL == 3) {
+        w[1] = ds_read_at<(O * PL + 1) * 1024>(base);
+        w[2] = ds_read_at<(O * PL + 2) * 1024>(base);
+    }
+}
+
+// Output tile O of one k-step: issue the reads of tile O + kDist, wait for tile O's (leaving
+// the younger ones in flight), six MFMAs (small terms first).
+template <int NTO, int PL, int O>
+__device__ __forceinline__ void tile_step(unsigned base, bf8 (&w)[kDist + 1][3], const bf8& bh,
+                                          const bf8& bm, const bf8& bl, fx4 (&out)[kMaxT]) {
+    if constexpr (O + kDist < NTO) read_tile<PL, O + kDist>(base, w[(O + kDist) % (kDist + 1)]);
+    constexpr int ahead = (NTO - 1 - O) < kDist ? (NTO - 1 - O) : kDist;
+    bf8(&c)[3] = w[O % (kDist + 1)];
+    lgkm_wait<ahead * PL>(c);
+    fx4 acc = out[O];
+    if constexpr (PL == 3) {
+        acc = mfma16(c[0], bl, acc);
+        acc = mfma16(c[1], bm, acc);
+        acc = mfma16(c[2], bh, acc);
+        acc = mfma16(c[1], bh, acc);
+        acc = mfma16(c[0], bm, acc);
+        acc = mfma16(c[0], bh, acc);
+    } else {
+        acc = mfma16(c[0], bh, acc);
+    }
+    out[O] = acc;
+}
+
+template <int NTO, int PL, int... O>
+__device__ __forceinline__ void tile_steps(std::integer_sequence<int, O...>, unsigned base,
+                                           bf8 (&w)[kDist + 1][3], const bf8& bh, const bf8& bm,
+                                           const bf8& bl, fx4 (&out)[kMaxT]) {
+    (tile_step<NTO, PL, O>(base, w, bh, bm, bl, out), ...);
+}
+
 // One pass (a layer's forward or backward MMA): out[o] += sum over the pass's k-steps of
 // Wpack[s][o] (x) in[2s..2s+1], NTO output tiles, chunk s streamed through the ring while chunk
 // s + 1 (or the next pass's first chunk) is in flight. `slab` (nullable) receives the input
@@ -179,7 +243,11 @@ __device__ __forceinline__ void k16_pass(const K16Args& a, Chunk cur, int ks, Ch
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
         if (s < ks) {
-            const unsigned char* buf = ring + slot * kSlotBytes;
+            const unsigned base = lds_addr(ring + slot * kSlotBytes) + lane * 16;
+            bf8 w[kDist + 1][3];
+            // the first weight tiles are in flight while the operand split and the DMA issue
+            read_tile<PL, 0>(base, w[0]);
+            if constexpr (NTO > 1) read_tile<PL, 1>(base, w[1]);
             Chunk n = nxt;
             if (s + 1 < ks) {
                 n = cur;
@@ -202,28 +270,12 @@ __device__ __forceinline__ void k16_pass(const K16Args& a, Chunk cur, int ks, Ch
                     bh[j] = (__bf16)x;
                 }
             }
-            const bf8* wp = (const bf8*)(buf + lane * 16);
-#pragma unroll
-            for (int o = 0; o < NTO; ++o) {
-                if (PL == 3) {
-                    const bf8 wh = wp[(o * 3 + 0) * 64], wm = wp[(o * 3 + 1) * 64], wl = wp[(o * 3 + 2) * 64];
-                    fx4 acc = out[o];
-                    acc = mfma16(wh, bl, acc);   // small terms first
-                    acc = mfma16(wm, bm, acc);
-                    acc = mfma16(wl, bh, acc);
-                    acc = mfma16(wm, bh, acc);
-                    acc = mfma16(wh, bm, acc);
-                    acc = mfma16(wh, bh, acc);
-                    out[o] = acc;
-                } else {
-                    out[o] = mfma16(wp[o * 64], bh, out[o]);
-                }
-            }
+            static_assert(kDist == 2, "prologue reads two tiles");
+            tile_steps<NTO, PL>(std::make_integer_sequence<int, NTO>{}, base, w, bh, bm, bl, out);
             dma_barrier();
             slot ^= 1;
         }
     }
-    (void)cur;
 }
 
 template <int PL>

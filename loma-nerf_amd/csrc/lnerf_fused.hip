@@ -1461,7 +1461,7 @@ __global__ void grad_reduce_kernel(ReduceArgs a) {
     }
 }
 
-inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+constexpr size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 struct Layout {
     int ht;                                   // hidden output tiles, rounded to 1/2/4/8
@@ -1480,6 +1480,7 @@ struct Layout {
     int ht16, ks16_f[kMaxLayers], ks16_b[kMaxLayers], to16_f[kMaxLayers], to16_b[kMaxLayers];
     size_t w16f_off[kMaxLayers], w16b_off[kMaxLayers], w16_total;   // u16
     size_t b16_total;                                                 // floats
+    size_t mask_total;                                                // u64 (k16 ReLU masks)
 };
 
 inline int pow2_tiles(int t) { return t <= 1 ? 1 : t <= 2 ? 2 : t <= 4 ? 4 : 8; }
@@ -1536,6 +1537,7 @@ void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S, bool train = tr
     y.b16_total = (size_t)L * 256;
     y.rpw = S >= kTileSamples ? 1 : kTileSamples / S;
     y.num_wg = (rays + y.rpw - 1) / y.rpw;
+    y.mask_total = train ? (size_t)y.num_wg * (L > 1 ? L - 1 : 0) * 8 * 64 : 0;
     y.blocks = y.num_wg * kWaves;
     off = 0;
     y.x_off = off; off += (size_t)y.blocks * kt[0] * 1024;
@@ -1602,7 +1604,8 @@ size_t fused_workspace_bytes(const lnerf_mlp& m, int rays, int S, bool train) {
     size_t f = align_up(y.pack_total, 64) + align_up((y.w6_total + 1) / 2, 64) +
                align_up(y.act_total, 64) + align_up(y.grad_total, 64) +
                align_up((size_t)y.num_wg, 64) + align_up(y.dwp_total, 64) + align_up(y.dbp_total, 64) +
-               64 + align_up((y.w16_total + 1) / 2, 64) + align_up(y.b16_total, 64);
+               64 + align_up((y.w16_total + 1) / 2, 64) + align_up(y.b16_total, 64) +
+               align_up(y.mask_total * 2, 64);
     return f * sizeof(float);
 }
 
@@ -1676,6 +1679,9 @@ void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws
     off += align_up((y.w16_total + 1) / 2, 64);
     p.b16 = base + off;
     off += align_up(y.b16_total, 64);
+    p.mask_g = (unsigned long long*)(base + off);
+    off += align_up(y.mask_total * 2, 64);
+
     p.x_off = y.x_off;
     p.ht16 = y.ht16;
     for (int l = 0; l < p.L; ++l) {

@@ -156,6 +156,7 @@ struct FusedPlan {
     unsigned short* w16;                 // packed planes, u16 offsets below
     size_t w16f_off[kMaxLayers], w16b_off[kMaxLayers];
     float* b16;                          // [L][256] zero-padded biases
+    unsigned long long* mask_g;          // [num_wg][L-1][8 waves][64 lanes] ReLU mask bits
 };
 
 bool fused_supported(const lnerf_mlp& mlp, int rays, int S, int input_mode, const char** why);

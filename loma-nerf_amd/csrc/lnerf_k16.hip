@@ -10,7 +10,8 @@
 //    = features 4(l >> 4) + i of each 16-feature tile), which is the next layer's B operand after
 //    a fixed permutation of the contraction order (phi below) baked into the weight packing;
 //  * the weights of one k-step (32 input features x every output tile, in the 3 bf16 planes of
-//    the bf16x6 split) stream through a 2-slot LDS ring by LDS-DMA, one barrier per k-step;
+//    the bf16x6 split) stream through a 3-slot LDS ring by LDS-DMA (two chunks in flight), one
+//    barrier per k-step;
 //  * while one wave of a SIMD issues its LDS reads, operand splits, slab stores, DMA pieces or
 //    epilogue, its partner's MFMAs keep the matrix core busy -- the latency hiding that the
 //    one-wave-per-SIMD kernel had to hand-schedule.
@@ -18,6 +19,9 @@
 // reads (lnerf_fused.hip slab_off): a wave owns one 16-sample half of a 32-sample block.
 #include "lnerf_composite.h"
 #include "lnerf_internal.h"
+
+#include <stddef.h>
+#include <stdio.h>
 
 #include <utility>
 
@@ -31,15 +35,33 @@ typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
 constexpr int kThreads = 512;
 constexpr int kWaves = 8;
 constexpr int kTile = comp::kTileSamples;     // 128 samples per workgroup
+constexpr int kMaxChunks = 2 * kMaxLayers * 8 + 2;   // <= 2 passes x 8 k-steps per layer + 2 end
 constexpr int kMaxT = 16;                     // 16-feature tiles per 256-wide layer
 constexpr int kSlotBytes = kMaxT * 3 * 1024;  // one k-step of a 256-output layer, 3 planes
-constexpr int kMaxMaskLayers = 8;
-constexpr int kOffMask = 2 * kSlotBytes;
-constexpr int kOffComp = kOffMask + kMaxMaskLayers * kWaves * 64 * 8;
-constexpr int kOffRay = kOffComp + kTile * comp::kCompFloats * 4;
+#ifndef LNERF_K16_AHEAD
+#define LNERF_K16_AHEAD 1
+#endif
+#ifndef LNERF_K16_LOADERS
+#define LNERF_K16_LOADERS 4
+#endif
+constexpr int kLoaders = LNERF_K16_LOADERS;   // waves that issue the weight DMA
+// timing experiments only (wrong results): drop the slab stores / the weight DMA after chunk 2
+#ifndef LNERF_K16_NOSTORE
+#define LNERF_K16_NOSTORE 0
+#endif
+#ifndef LNERF_K16_NODMA
+#define LNERF_K16_NODMA 0
+#endif
+// chunks in flight while one computes: 1 (waited with vmcnt(0)) measured faster than 2 (a 3-slot
+// ring waited with vmcnt(pending)): 1.96-2.00 vs 2.16 ms
+constexpr int kAhead = LNERF_K16_AHEAD;
+constexpr int kSlots = kAhead + 1;            // ring slots
+constexpr int kOffComp = 3 * kSlotBytes;      // room for the deepest ring (kAhead = 2)
+constexpr int kCompBytes = 2688 * 4;          // composite_tile's scratch (comp[0, 2688))
+constexpr int kOffRay = kOffComp + kCompBytes;
 constexpr int kOffBias = kOffRay + kTile * 4;
-constexpr int kLdsBytes = kOffBias + 2 * 256 * 4;
-static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
+constexpr int kLdsBytes = kOffBias + 3 * 256 * 4;   // + a 3-slot ring of layer biases
+static_assert(kLdsBytes + 1024 <= 160 * 1024, "LDS budget (+1 KiB for the profiling build)");
 
 struct K16Args {
     int L;
@@ -50,6 +72,10 @@ struct K16Args {
     const unsigned short* w16;
     size_t wf_off[kMaxLayers], wb_off[kMaxLayers];   // u16 offsets
     const float* b16;                                // [L][256] zero-padded biases
+    unsigned long long* mask_g;                      // [wg][L-1][wave][lane] ReLU mask bits
+    // the chunk stream (k16_launch): per chunk {u16 offset in w16, (bytes / 1024) | (bias layer + 1)
+    // << 16}, zero past the end. Read with scalar loads from the kernel-argument segment.
+    unsigned chunk_tab[2 * kMaxChunks];
     float* act;
     size_t act_off[kMaxLayers];
     size_t x_off;
@@ -72,76 +98,104 @@ struct K16Args {
 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
+// ---- optional in-kernel phase timing (-DLNERF_PROF=1, never in the product build): per-wave
+// s_memtime deltas, lane 0 accumulating in LDS, summed into g_k16_prof at the end.
+#ifndef LNERF_PROF
+#define LNERF_PROF 0
+#endif
+#if LNERF_PROF
+enum { kPfPE, kPfFwd, kPfFwdEpi, kPfBar, kPfComp, kPfBwd, kPfBwdEpi, kPfTail, kPfTotal, kPfVm, kPfN };
+__device__ unsigned long long g_k16_prof[16];
+__device__ __forceinline__ unsigned long long* prof_slots() {
+    __shared__ unsigned long long sl[kWaves][16];
+    return &sl[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)][0];
+}
+#define PROF_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define PROF_ADD(cat, t0) \
+    do { if ((threadIdx.x & 63) == 0) prof_slots()[cat] += __builtin_amdgcn_s_memtime() - (t0); } while (0)
+#else
+#define PROF_T(v)
+#define PROF_ADD(cat, t0)
+#endif
+
 // Input feature of k-step s held in element j of a lane in lane group g (the B operand's
 // k = 8g + j): tile 2s + (j >> 2), register j & 3 of that lane.
 __host__ __device__ __forceinline__ int phi(int s, int g, int j) {
     return 32 * s + 16 * (j >> 2) + 4 * g + (j & 3);
 }
 
-// One chunk of packed weights (one k-step of one pass) and, for the first chunk of a forward
-// pass, the layer's biases.
-struct Chunk {
-    const unsigned short* src;
+// Chunk `ci` of the kernel's stream (forward passes 0..L-1, then (training) backward L-1..1 and
+// backward 0 when d_x is wanted), from K16Args::chunk_tab through the kernel-argument segment
+// pointer: a scalar load at a dynamic offset (indexing the by-value argument itself would copy
+// it to scratch; a vector load would sit in vmcnt behind the in-flight DMA).
+struct ChunkT {
+    const unsigned short* src;   // nullptr: past the last chunk
     int bytes;
-    const float* bias;
-    int bias_slot;
+    int bias;                    // layer whose biases ride with this chunk, -1: none
 };
 
-__device__ __forceinline__ Chunk pass_chunk(const K16Args& a, bool fwd, int l, int s) {
-    const int to = fwd ? a.to_f[l] : a.to_b[l];
-    const size_t per = (size_t)to * a.planes * 512;   // u16 per chunk
-    Chunk c;
-    c.src = a.w16 + (fwd ? a.wf_off[l] : a.wb_off[l]) + (size_t)s * per;
-    c.bytes = (int)(per * 2);
-    c.bias = (fwd && s == 0) ? a.b16 + (size_t)l * 256 : nullptr;
-    c.bias_slot = l & 1;
-    return c;
+__device__ __forceinline__ ChunkT chunk_at(const K16Args& a, int ci) {
+    const __attribute__((address_space(4))) unsigned* t =
+        (const __attribute__((address_space(4))) unsigned*)((const __attribute__((address_space(4))) char*)
+                                                                __builtin_amdgcn_kernarg_segment_ptr() +
+                                                            offsetof(K16Args, chunk_tab)) + 2 * ci;
+    const unsigned off = t[0], e = t[1];
+    const int bytes = (int)(e & 0xFFFFu) * 1024;
+    return ChunkT{bytes ? a.w16 + off : nullptr, bytes, (int)(e >> 16) - 1};
 }
 
-__device__ __forceinline__ Chunk no_chunk() { return Chunk{nullptr, 0, nullptr, 0}; }
-
-// The first chunk of the pass that follows pass (fwd, l) in the kernel's order: forward 0..L-1,
-// then (training) backward L-1..1, and backward 0 when d_x is wanted.
-__device__ __forceinline__ Chunk next_pass_chunk(const K16Args& a, bool fwd, int l) {
-    int nl;
-    bool nf;
-    if (fwd) {
-        if (l + 1 < a.L) return pass_chunk(a, true, l + 1, 0);
-        if (!a.want_grad) return no_chunk();
-        nf = false;
-        nl = a.L - 1;
-    } else {
-        nf = false;
-        nl = l - 1;
-    }
-    if (nl < 0 || (nl == 0 && !a.d_x)) return no_chunk();
-    return pass_chunk(a, nf, nl, 0);
-}
-
-// LDS-DMA (global_load_lds_dwordx4) of `bytes` (a multiple of 1 KiB) into `dst`: 8 KiB per
-// round of the workgroup, each wave instruction 1 KiB (lane-linear).
-__device__ __forceinline__ void dma_chunk(const Chunk& c, unsigned char* dst, float* bias_lds) {
+// LDS-DMA (global_load_lds_dwordx4) of a chunk into its ring slot: 8 KiB per round of the
+// workgroup, each wave instruction 1 KiB (lane-linear); the last wave also stages the biases a
+// first forward chunk carries (bias ring slot l % 3). Returns the instructions this wave issued
+// (what a later vmcnt must leave outstanding).
+__device__ __forceinline__ int dma_chunk(const K16Args& a, const ChunkT& c, unsigned char* dst,
+                                         float* bias_ring) {
     const int tid = threadIdx.x, wave = wave_id();
-    for (int off = wave * 1024; off < c.bytes; off += kThreads * 16) {
+    int n = 0;
+    if (!c.src) return 0;
+    // loader waves 0..kLoaders-1 (waves w and w+4 share a SIMD: with 4 loaders each SIMD keeps
+    // one wave free of DMA issue to feed the matrix core)
+    if (wave >= kLoaders) return 0;
+    for (int off = wave * 1024; off < c.bytes; off += kLoaders * 1024) {
         const char* g = (const char*)c.src + off + (tid & 63) * 16;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                          (__attribute__((address_space(3))) void*)(dst + off), 16, 0, 0);
+        ++n;
     }
-    if (c.bias && wave == kWaves - 1) {
-        const float* g = c.bias + (tid & 63) * 4;
+    if (c.bias >= 0 && wave == kLoaders - 1) {
+        const float* g = a.b16 + (size_t)c.bias * 256 + (tid & 63) * 4;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                         (__attribute__((address_space(3))) void*)(bias_lds + c.bias_slot * 256),
+                                         (__attribute__((address_space(3))) void*)(bias_ring + (c.bias % 3) * 256),
                                          16, 0, 0);
+        ++n;
     }
+    return n;
 }
 
-// Every wave's LDS-DMA has landed and every wave is done with the slot it read:
-// vmcnt(0) (loads and stores share the counter) + s_barrier.
-__device__ __forceinline__ void dma_barrier() {
+// The chunk the next k-step reads has landed (this wave's pieces: vector-memory loads return in
+// issue order, so at most `pending` outstanding -- the pieces of the chunk after it, issued
+// later -- means every older load is done, whatever the stores in between), then s_barrier:
+// every wave's pieces are in LDS and every wave is done with the slot the next DMA overwrites.
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void dma_barrier(int pending) {
+    PROF_T(t0);
     asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), expcnt(7), lgkmcnt(15)
+    switch (pending) {
+        case 0: vm_wait<0>(); break;
+        case 1: vm_wait<1>(); break;
+        case 2: vm_wait<2>(); break;
+        case 3: vm_wait<3>(); break;
+        case 4: vm_wait<4>(); break;
+        case 5: vm_wait<5>(); break;
+        default: vm_wait<6>(); break;
+    }
+    PROF_ADD(kPfVm, t0);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    PROF_ADD(kPfBar, t0);
 }
 
 __device__ __forceinline__ fx4 mfma16(const bf8& a, const bf8& b, fx4 c) {
@@ -231,32 +285,31 @@ __device__ __forceinline__ void tile_steps(std::integer_sequence<int, O...>, uns
 }
 
 // One pass (a layer's forward or backward MMA): out[o] += sum over the pass's k-steps of
-// Wpack[s][o] (x) in[2s..2s+1], NTO output tiles, chunk s streamed through the ring while chunk
-// s + 1 (or the next pass's first chunk) is in flight. `slab` (nullable) receives the input
-// tiles (the A_{l-1} or G_l slab of this wave's half-block).
+// Wpack[s][o] (x) in[2s..2s+1], NTO output tiles. Chunk ci is read from ring slot ci % 3 while
+// chunks ci+1 (issued one k-step earlier) and ci+2 (issued here) land. `slab` (nullable)
+// receives the input tiles (the A_{l-1} or G_l slab of this wave's half-block).
 template <int NTO, int PL>
-__device__ __forceinline__ void k16_pass(const K16Args& a, Chunk cur, int ks, Chunk nxt, int& slot,
-                                         unsigned char* ring, float* bias_lds, const fx4 (&in)[kMaxT],
-                                         fx4 (&out)[kMaxT], float* __restrict__ slab) {
+__device__ __forceinline__ void k16_pass(const K16Args& a, int ks, int& ci, unsigned char* ring,
+                                         float* bias_ring, const fx4 (&in)[kMaxT], fx4 (&out)[kMaxT],
+                                         float* __restrict__ slab) {
     const int lane = threadIdx.x & 63;
-    const size_t per = (size_t)NTO * PL * 512;
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
         if (s < ks) {
-            const unsigned base = lds_addr(ring + slot * kSlotBytes) + lane * 16;
+            const unsigned base = lds_addr(ring + (ci % kSlots) * kSlotBytes) + lane * 16;
+            // DMA of chunk ci+AHEAD first (its table entry is a scalar load the compiler waits for
+            // with lgkmcnt(0), which would also wait for the fragment reads), then the first
+            // weight tiles, in flight while the slab stores and the operand split issue
+            const int pending = (LNERF_K16_NODMA && ci >= 2)
+                                    ? 0
+                                    : dma_chunk(a, chunk_at(a, ci + kAhead),
+                                                ring + ((ci + kAhead) % kSlots) * kSlotBytes, bias_ring) *
+                                          (kAhead - 1);
             bf8 w[kDist + 1][3];
-            // the first weight tiles are in flight while the operand split and the DMA issue
             read_tile<PL, 0>(base, w[0]);
             if constexpr (NTO > 1) read_tile<PL, 1>(base, w[1]);
-            Chunk n = nxt;
-            if (s + 1 < ks) {
-                n = cur;
-                n.src = cur.src + (size_t)(s + 1) * per;
-                n.bias = nullptr;
-            }
-            if (n.src) dma_chunk(n, ring + (slot ^ 1) * kSlotBytes, bias_lds);
-            if (slab) store_slab_step(slab + s * 1024, in[2 * s], in[2 * s + 1]);
-            bf8 bh, bm, bl;
+            if (slab && !LNERF_K16_NOSTORE) store_slab_step(slab + s * 1024, in[2 * s], in[2 * s + 1]);
+            bf8 bh, bm = {}, bl = {};
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const float x = j < 4 ? in[2 * s][j] : in[2 * s + 1][j - 4];
@@ -272,21 +325,43 @@ __device__ __forceinline__ void k16_pass(const K16Args& a, Chunk cur, int ks, Ch
             }
             static_assert(kDist == 2, "prologue reads two tiles");
             tile_steps<NTO, PL>(std::make_integer_sequence<int, NTO>{}, base, w, bh, bm, bl, out);
-            dma_barrier();
-            slot ^= 1;
+            dma_barrier(pending);
+            ++ci;
         }
     }
 }
 
 template <int PL>
-__device__ __forceinline__ void k16_pass_n(const K16Args& a, Chunk cur, int ks, Chunk nxt, int& slot,
-                                           unsigned char* ring, float* bias_lds, int nto,
-                                           const fx4 (&in)[kMaxT], fx4 (&out)[kMaxT], float* slab) {
-    if (nto <= 1) k16_pass<1, PL>(a, cur, ks, nxt, slot, ring, bias_lds, in, out, slab);
-    else if (nto <= 2) k16_pass<2, PL>(a, cur, ks, nxt, slot, ring, bias_lds, in, out, slab);
-    else if (nto <= 4) k16_pass<4, PL>(a, cur, ks, nxt, slot, ring, bias_lds, in, out, slab);
-    else if (nto <= 8) k16_pass<8, PL>(a, cur, ks, nxt, slot, ring, bias_lds, in, out, slab);
-    else k16_pass<16, PL>(a, cur, ks, nxt, slot, ring, bias_lds, in, out, slab);
+__device__ __forceinline__ void k16_pass_n(const K16Args& a, int ks, int& ci, unsigned char* ring,
+                                           float* bias_ring, int nto, const fx4 (&in)[kMaxT],
+                                           fx4 (&out)[kMaxT], float* slab) {
+    if (nto <= 1) k16_pass<1, PL>(a, ks, ci, ring, bias_ring, in, out, slab);
+    else if (nto <= 2) k16_pass<2, PL>(a, ks, ci, ring, bias_ring, in, out, slab);
+    else if (nto <= 4) k16_pass<4, PL>(a, ks, ci, ring, bias_ring, in, out, slab);
+    else if (nto <= 8) k16_pass<8, PL>(a, ks, ci, ring, bias_ring, in, out, slab);
+    else k16_pass<16, PL>(a, ks, ci, ring, bias_ring, in, out, slab);
+}
+
+// The layer's biases in the accumulator layout (fx4 = 4 consecutive features of a lane group),
+// from its bias ring slot: ds_read_b128 outside the compiler's waitcnt bookkeeping (a plain LDS
+// read would make it wait vmcnt(0) for the in-flight weight DMA), one dependent wait per tile.
+template <int N>
+__device__ __forceinline__ void lgkm_wait4(fx4& v) {
+    asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(v) : "n"(N));
+}
+template <int OFF>
+__device__ __forceinline__ fx4 ds_read_f4(unsigned addr) {
+    fx4 r;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+    return r;
+}
+template <int NT, int... O>
+__device__ __forceinline__ void bias_read(std::integer_sequence<int, O...>, unsigned addr, fx4 (&b)[kMaxT]) {
+    ((b[O] = ds_read_f4<O * 64>(addr)), ...);
+}
+template <int NT, int... O>
+__device__ __forceinline__ void bias_wait(std::integer_sequence<int, O...>, fx4 (&b)[kMaxT]) {
+    (lgkm_wait4<NT - 1 - O>(b[O]), ...);
 }
 
 __device__ __forceinline__ void zero_tiles(fx4 (&t)[kMaxT]) {
@@ -300,10 +375,9 @@ template <int HT, int PL>
 __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
     __shared__ __attribute__((aligned(16))) unsigned char lds[kLdsBytes];
     unsigned char* ring = lds;
-    unsigned long long* masks = (unsigned long long*)(lds + kOffMask);
     float* comp = (float*)(lds + kOffComp);
     float* rayloss = (float*)(lds + kOffRay);
-    float* bias_lds = (float*)(lds + kOffBias);
+    float* bias_ring = (float*)(lds + kOffBias);
 
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id(), g = lane >> 4, n = lane & 15;
     const int wg = blockIdx.x;
@@ -314,6 +388,10 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
     const size_t blk = (size_t)wg * 4 + (wave >> 1);   // 32-sample slab block
     const int half = wave & 1;
     const bool st = a.want_grad != 0;
+#if LNERF_PROF
+    if (lane < 16) prof_slots()[lane] = 0;
+    PROF_T(t_start);
+#endif
 
     fx4 act[kMaxT], out[kMaxT];
     zero_tiles(act);
@@ -364,48 +442,56 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
     }
     __syncthreads();   // the first DMA overwrites the scratch
 
-    int slot = 0;
-    {
-        const Chunk c0 = pass_chunk(a, true, 0, 0);
-        dma_chunk(c0, ring, bias_lds);
-        dma_barrier();
-    }
+    int ci = 0;   // chunk stream position (chunk_at)
+    dma_chunk(a, chunk_at(a, 0), ring, bias_ring);
+    dma_barrier(kAhead == 2 ? dma_chunk(a, chunk_at(a, 1), ring + kSlotBytes, bias_ring) : 0);
+    PROF_ADD(kPfPE, t_start);
+    // ReLU mask bits of this wave, per hidden layer: [L-1][lane] u64
+    unsigned long long* mask_w = a.mask_g + ((size_t)wg * (a.L - 1) * kWaves + wave) * 64 + lane;
 
     // ---- forward ----
     for (int l = 0; l < a.L; ++l) {
-        zero_tiles(out);
         float* slab = !st ? nullptr
                           : (l == 0 ? a.act + a.x_off + blk * (size_t)(a.kt[0] * 1024)
                                     : a.act + a.act_off[l - 1] + blk * (size_t)(a.kt[l] * 1024)) +
                                 half * 512;
-        const Chunk c = pass_chunk(a, true, l, 0);
-        const Chunk nx = next_pass_chunk(a, true, l);
-        const float* bl = bias_lds + (l & 1) * 256;
+        zero_tiles(out);
+        const unsigned bl = lds_addr(bias_ring + (l % 3) * 256) + g * 16;
         if (l < a.L - 1) {
-            k16_pass<HT, PL>(a, c, a.ks_f[l], nx, slot, ring, bias_lds, act, out, slab);
-            // bias after the sum (nerf.py:98,125), ReLU (nerf.py:141-144), mask bits
+            PROF_T(t_f);
+            k16_pass<HT, PL>(a, a.ks_f[l], ci, ring, bias_ring, act, out, slab);
+            PROF_ADD(kPfFwd, t_f);
+            PROF_T(t_fe);
+            // bias after the sum (nerf.py:98,125), ReLU (nerf.py:141-144) and its mask bits
+            fx4 bv[kMaxT];
+            bias_read<HT>(std::make_integer_sequence<int, HT>{}, bl, bv);
+            bias_wait<HT>(std::make_integer_sequence<int, HT>{}, bv);
             unsigned long long mb = 0ull;
 #pragma unroll
             for (int o = 0; o < HT; ++o) {
-                const fx4 b4 = *(const fx4*)(bl + 16 * o + 4 * g);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const float v = out[o][i] + b4[i];
+                    const float v = out[o][i] + bv[o][i];
                     const bool pos = v > 0.0f;
                     act[o][i] = pos ? v : 0.0f;
                     mb |= (pos ? 1ull : 0ull) << (4 * o + i);
                 }
             }
-            masks[((size_t)l * kWaves + wave) * 64 + lane] = mb;
+            if (st) mask_w[(size_t)l * kWaves * 64] = mb;
+            PROF_ADD(kPfFwdEpi, t_fe);
         } else {
-            k16_pass<1, PL>(a, c, a.ks_f[l], nx, slot, ring, bias_lds, act, out, slab);
+            k16_pass<1, PL>(a, a.ks_f[l], ci, ring, bias_ring, act, out, slab);
+            fx4 bv[kMaxT];
+            bias_read<1>(std::make_integer_sequence<int, 1>{}, bl, bv);
+            bias_wait<1>(std::make_integer_sequence<int, 1>{}, bv);
             // head pre-activations: features 0..3 = registers 0..3 of lane group 0
             if (g == 0) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) comp[ls * 4 + i] = out[0][i] + bl[i];
+                for (int i = 0; i < 4; ++i) comp[ls * 4 + i] = out[0][i] + bv[0][i];
             }
         }
     }
+    PROF_T(t_c);
     __syncthreads();
 
     // ---- rendering + loss + rendering reverse (one thread per sample, scans along rays) ----
@@ -416,6 +502,7 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
         for (int r = 0; r < a.rpw; ++r) lsum = lsum + rayloss[r];
         a.loss_part[wg] = lsum;
     }
+    PROF_ADD(kPfComp, t_c);
     if (!st) return;
 
     // ---- reverse chain: G_{L-1} from the head, G_{l-1} = (W_l G_l) * 1[A_{l-1} > 0] ----
@@ -428,21 +515,24 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
     for (int l = a.L - 1; l >= 1; --l) {
         zero_tiles(out);
         float* slab = a.grad + a.grad_off[l] + blk * (size_t)(a.nt[l] * 1024) + half * 512;
-        k16_pass<HT, PL>(a, pass_chunk(a, false, l, 0), a.ks_b[l], next_pass_chunk(a, false, l), slot,
-                         ring, bias_lds, act, out, slab);
-        const unsigned long long mb = masks[((size_t)(l - 1) * kWaves + wave) * 64 + lane];
+        PROF_T(t_b);
+        const unsigned long long mb = mask_w[(size_t)(l - 1) * kWaves * 64];   // in flight over the pass
+        k16_pass<HT, PL>(a, a.ks_b[l], ci, ring, bias_ring, act, out, slab);
+        PROF_ADD(kPfBwd, t_b);
+        PROF_T(t_be);
 #pragma unroll
         for (int o = 0; o < HT; ++o)
 #pragma unroll
             for (int i = 0; i < 4; ++i) act[o][i] = ((mb >> (4 * o + i)) & 1ull) ? out[o][i] : 0.0f;
+        PROF_ADD(kPfBwdEpi, t_be);
     }
+    PROF_T(t_t);
     // act holds G_0
     float* g0 = a.grad + a.grad_off[0] + blk * (size_t)(a.nt[0] * 1024) + half * 512;
     if (a.d_x) {
         // d_layer_input = G_0 W_0^T (ENCODED mode); the pass also writes G_0's slab
         zero_tiles(out);
-        k16_pass_n<PL>(a, pass_chunk(a, false, 0, 0), a.ks_b[0], no_chunk(), slot, ring, bias_lds,
-                       a.to_b[0], act, out, g0);
+        k16_pass_n<PL>(a, a.ks_b[0], ci, ring, bias_ring, a.to_b[0], act, out, g0);
         if (valid) {
 #pragma unroll
             for (int o = 0; o < kMaxT; ++o)
@@ -459,6 +549,11 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
         for (int s = 0; s < 8; ++s)
             if (s < a.ks_b[0]) store_slab_step(g0 + s * 1024, act[2 * s], act[2 * s + 1]);
     }
+#if LNERF_PROF
+    PROF_ADD(kPfTail, t_t);
+    PROF_ADD(kPfTotal, t_start);
+    if (lane < kPfN) atomicAdd(&g_k16_prof[lane], prof_slots()[lane]);
+#endif
 }
 
 // ---- weight packing: per layer and pass, chunk s = [o][plane][lane 64][8 x bf16] -----------
@@ -513,7 +608,6 @@ __global__ void pack16_kernel(Pack16Args a, int l) {
 
 bool k16_supported(const FusedPlan& p) {
     if (p.x6 != 3 && p.x6 != 1) return false;
-    if (p.L - 1 > kMaxMaskLayers) return false;
     if (p.n[p.L - 1] > 16) return false;       // head: one 16-wide output tile
     return true;
 }
@@ -563,6 +657,7 @@ void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lner
     a.k0 = p.k[0];
     a.w16 = p.w16;
     a.b16 = p.b16;
+    a.mask_g = p.mask_g;
     a.act = p.act;
     a.x_off = p.x_off;
     a.grad = p.grad;
@@ -585,6 +680,23 @@ void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lner
     a.seed = seed;
     a.want_grad = want_grad ? 1 : 0;
     a.planes = p.x6;
+    // the chunk stream: forward 0..L-1, backward L-1..1 (training), backward 0 (d_x)
+    {
+        int ci = 0;
+        auto add = [&](bool fwd, int l) {
+            const int ks = fwd ? a.ks_f[l] : a.ks_b[l], to = fwd ? a.to_f[l] : a.to_b[l];
+            const size_t per = (size_t)to * a.planes * 512;   // u16
+            for (int s2 = 0; s2 < ks; ++s2, ++ci) {
+                a.chunk_tab[2 * ci] = (unsigned)((fwd ? a.wf_off[l] : a.wb_off[l]) + (size_t)s2 * per);
+                a.chunk_tab[2 * ci + 1] = (unsigned)(per * 2 / 1024) | ((fwd && s2 == 0 ? l + 1 : 0) << 16);
+            }
+        };
+        for (int l = 0; l < p.L; ++l) add(true, l);
+        if (want_grad)
+            for (int l = p.L - 1; l >= (a.d_x ? 0 : 1); --l) add(false, l);
+        // two zero entries past the end (the kernel looks two chunks ahead): a{} zeroed them
+    }
+    static_assert(sizeof(K16Args) <= 4096, "kernel arguments");
 #define LNERF_K16_LAUNCH(HT)                                                              \
     if (p.x6 == 3) k16_fwd_bwd_kernel<HT, 3><<<p.num_wg, kThreads, 0, s>>>(a);            \
     else k16_fwd_bwd_kernel<HT, 1><<<p.num_wg, kThreads, 0, s>>>(a);
@@ -596,6 +708,20 @@ void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lner
         default: LNERF_K16_LAUNCH(16) break;
     }
 #undef LNERF_K16_LAUNCH
+#if LNERF_PROF
+    if (want_grad) {
+        unsigned long long h[16] = {};
+        (void)hipStreamSynchronize(s);
+        (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_k16_prof), sizeof(h));
+        const char* names[] = {"pe", "fwd_pass", "fwd_epilogue", "barrier", "composite", "bwd_pass",
+                               "bwd_epilogue", "tail", "total", "vmcnt_wait"};
+        fprintf(stderr, "LNERF_PROF k16 per-wave cycles:");
+        for (int i = 0; i < kPfN; ++i) fprintf(stderr, " %s=%.0f", names[i], h[i] / ((double)p.num_wg * kWaves));
+        fprintf(stderr, "\n");
+        unsigned long long z[16] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_k16_prof), z, sizeof(z));
+    }
+#endif
 }
 
 }  // namespace lnerf

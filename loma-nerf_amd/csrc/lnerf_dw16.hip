@@ -1,0 +1,275 @@
+// lnerf_dw16.hip -- k2 on wave pairs: dW_l = sum_s A_{l-1}[s]^T G_l[s] and db_l = sum_s G_l[s]
+// from the slabs k1 wrote, bf16x6 (fp32-accurate) on v_mfma_f32_32x32x16_bf16, two waves per
+// SIMD.
+//
+// Reference: the weight/bias adjoints of nerf.py's reverse pass (reverse_diff.py:492-559;
+// dW_l += A_{l-1}^T G_l, db_l += sum_rows G_l). One workgroup (8 waves)
+// streams a contiguous range of 16-sample half-blocks of one layer:
+//  * global -> registers: the half-block's A rows (kt*32) and G rows (nt*32), 64 B per row, read
+//    as fully coalesced 16-B loads two half-blocks ahead (no LDS staging of fp32);
+//  * split once, cooperatively: every value is split into its hi/mid/lo bf16 planes exactly
+//    once per workgroup and written to a double-buffered LDS plane image [plane][row][16 samples]
+//    (the MFMA operand layout: 8 consecutive samples of a row = one 16-B fragment);
+//  * each wave owns a 64 x 128 block of the layer's output (2 x 4 tiles of 32 x 32, 128
+//    accumulator registers) and runs 6 MFMAs per tile pair and half-block;
+//  * db from the same registers (per-row partial sums, reduced in LDS at the end);
+//  * partials per split, summed in order by grad_reduce_kernel (deterministic, no atomics).
+#include "lnerf_internal.h"
+
+namespace lnerf {
+
+namespace {
+
+typedef float fx4 __attribute__((ext_vector_type(4)));
+typedef float fx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+
+// timing experiments only (wrong results): skip the MFMAs / the slab loads
+#ifndef LNERF_DW16_NOMMA
+#define LNERF_DW16_NOMMA 0
+#endif
+#ifndef LNERF_DW16_NOLOAD
+#define LNERF_DW16_NOLOAD 0
+#endif
+
+constexpr int kThreads = 512;
+constexpr int kRows = 512;                  // A rows [0, 256) and G rows [256, 512) of the image
+constexpr int kPlaneBytes = kRows * 32;     // one plane of a half-block: [row][16 samples] bf16
+constexpr int kImageBytes = 3 * kPlaneBytes;
+constexpr int kLdsBytes = 2 * kImageBytes;  // double-buffered (96 KiB)
+
+struct Dw16Args {
+    int kt[kMaxLayers], nt[kMaxLayers];
+    const float* act;
+    size_t a_off[kMaxLayers];   // A_{l-1} slab base per layer (X slab for l = 0)
+    const float* grad;
+    size_t g_off[kMaxLayers];
+    int blocks;                 // 32-sample blocks
+    int splits[kMaxLayers];
+    int nl;                     // layers in the launch
+    int lid[kMaxLayers];
+    int wg_off[kMaxLayers + 1]; // first workgroup of the i-th layer
+    float* dw_part;
+    size_t dwp_off[kMaxLayers];
+    float* db_part;
+    size_t dbp_off[kMaxLayers];
+};
+
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+// Address of the 16 B that thread t loads in round i (0..3) of half-block hb: image row
+// r = 128 i + t / 4 (A rows below 256, G rows from 256), samples 4 (t % 4) .. +3. A slab block
+// is [tile][half][32 rows][16 samples]; a half-block is one half of one 32-sample block.
+__device__ __forceinline__ const fx4* row_src(const Dw16Args& a, int l, int hb, int i, bool& ok) {
+    const int t = threadIdx.x, r = 128 * i + (t >> 2), q = t & 3;
+    const int blk = hb >> 1, half = hb & 1;
+    const bool isA = r < 256;
+    const int rr = isA ? r : r - 256;
+    const int tiles = isA ? a.kt[l] : a.nt[l];
+    ok = (rr >> 5) < tiles;
+    const int rc = ok ? rr : (rr & 31);   // a valid row of tile 0 when past the layer's tiles
+    const float* base = isA ? a.act + a.a_off[l] : a.grad + a.g_off[l];
+    return (const fx4*)(base + (size_t)blk * tiles * 1024 + (rc >> 5) * 1024 + half * 512 + (rc & 31) * 16 + 4 * q);
+}
+
+struct Loads {
+    fx4 v[4];
+};
+
+// Always four loads (rows past the layer's tiles and half-blocks past the split read a valid
+// address and are zeroed), so the compiler's vmcnt for them is exact.
+__device__ __forceinline__ void issue_loads(const Dw16Args& a, int l, int hb, int hb_end, Loads& L) {
+    const bool in = hb < hb_end;
+    const int hbc = in ? hb : max(0, hb_end - 1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        bool ok;
+        const fx4* p = row_src(a, l, hbc, i, ok);
+        const fx4 v = LNERF_DW16_NOLOAD ? fx4{1.0f, 2.0f, 3.0f, (float)i} : __builtin_nontemporal_load(p);
+        L.v[i] = (ok && in) ? v : fx4{0.0f, 0.0f, 0.0f, 0.0f};
+    }
+}
+
+// x = hi + mid + lo, round-to-nearest bf16 of each remainder (every remainder is exact in f32).
+__device__ __forceinline__ void split4(const fx4& x, bf4& h, bf4& m, bf4& lo) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const __bf16 hh = (__bf16)x[e];
+        const float r = x[e] - (float)hh;
+        const __bf16 mm = (__bf16)r;
+        h[e] = hh;
+        m[e] = mm;
+        lo[e] = (__bf16)(r - (float)mm);
+    }
+}
+
+// Split round i of the thread's values into the plane image (8 B per plane and row).
+__device__ __forceinline__ void write_planes_row(const fx4& v, int i, unsigned char* img) {
+    const int t = threadIdx.x, q = t & 3;
+    const int r = 128 * i + (t >> 2);
+    bf4 h, m, lo;
+    split4(v, h, m, lo);
+    unsigned char* p = img + r * 32 + q * 8;
+    *(bf4*)(p) = h;
+    *(bf4*)(p + kPlaneBytes) = m;
+    *(bf4*)(p + 2 * kPlaneBytes) = lo;
+}
+
+__device__ __forceinline__ void write_planes(const Loads& L, unsigned char* img) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) write_planes_row(L.v[i], i, img);
+}
+
+__device__ __forceinline__ fx16 mfma32(const bf8& a, const bf8& b, fx16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// The wave's 2 x 4 tile block on one half-block image (per 32-row tile a fragment is one
+// ds_read_b128 per plane; lane: row l & 31, samples 8 (l >> 5) .. +7), with the split of the
+// next half-block interleaved: round j of it beside output column tile j, so the VALU split
+// issues under the MFMAs. Branch-free (ACTIVE is a template parameter; past the split's last
+// half-block the zeroed loads land in the idle image buffer) so the scheduler can overlap it.
+template <bool ACTIVE>
+__device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int g0, fx16 (&acc)[2][4],
+                                          const Loads& nl, unsigned char* nxt) {
+    const int lane = threadIdx.x & 63, fo = (lane & 31) * 32 + (lane >> 5) * 16;
+    bf8 ap[2][3];
+    if constexpr (ACTIVE) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) ap[i][p] = *(const bf8*)(img + p * kPlaneBytes + (a0 + 32 * i) * 32 + fo);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        write_planes_row(nl.v[j], j, nxt);
+        if constexpr (ACTIVE) {
+            bf8 gp[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) gp[p] = *(const bf8*)(img + p * kPlaneBytes + (256 + g0 + 32 * j) * 32 + fo);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                fx16 c = acc[i][j];
+                c = mfma32(ap[i][0], gp[2], c);   // small terms first
+                c = mfma32(ap[i][1], gp[1], c);
+                c = mfma32(ap[i][2], gp[0], c);
+                c = mfma32(ap[i][1], gp[0], c);
+                c = mfma32(ap[i][0], gp[1], c);
+                c = mfma32(ap[i][0], gp[0], c);
+                acc[i][j] = c;
+            }
+        }
+    }
+}
+
+// The half-block loop of one split: L0 holds hb0 (already in the image), L1 hb0 + 1.
+template <bool ACTIVE>
+__device__ __forceinline__ void hb_loop(const Dw16Args& a, int l, int hb0, int hb1, int a0, int g0,
+                                        fx16 (&acc)[2][4], Loads& L0, Loads& L1, float (&dbs)[2],
+                                        unsigned char* lds) {
+    for (int hb = hb0; hb < hb1; ++hb) {
+        const int cur = (hb - hb0) & 1;
+        // L1 holds hb + 1 (zeros past the end); L0 receives hb + 2
+        issue_loads(a, l, hb + 2, hb1, L0);
+        dbs[0] += (L1.v[2][0] + L1.v[2][1]) + (L1.v[2][2] + L1.v[2][3]);
+        dbs[1] += (L1.v[3][0] + L1.v[3][1]) + (L1.v[3][2] + L1.v[3][3]);
+        block_mma<ACTIVE>(lds + cur * kImageBytes, a0, g0, acc, L1, lds + (cur ^ 1) * kImageBytes);
+        __syncthreads();
+        Loads t = L0;
+        L0 = L1;
+        L1 = t;
+    }
+}
+
+__global__ void __launch_bounds__(kThreads, 1) dw16_kernel(Dw16Args a) {
+    __shared__ __attribute__((aligned(16))) unsigned char lds[kLdsBytes];
+    int li = 0;
+    while (li + 1 < a.nl && (int)blockIdx.x >= a.wg_off[li + 1]) ++li;
+    const int l = a.lid[li], sp = blockIdx.x - a.wg_off[li];
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+    const int KT = a.kt[l], NT = a.nt[l];
+    // wave block: in rows [a0, a0 + 64), out rows [g0, g0 + 128)
+    const int nbg = (NT + 3) >> 2, nblk = ((KT + 1) >> 1) * nbg;
+    const bool active = wave < nblk && !LNERF_DW16_NOMMA;
+    const int a0 = active ? (wave / nbg) * 64 : 0, g0 = active ? (wave % nbg) * 128 : 0;
+    // half-block range of this split
+    const int hbs = 2 * a.blocks, splits = a.splits[l];
+    const int per = (hbs + splits - 1) / splits;
+    const int hb0 = min(hbs, sp * per), hb1 = min(hbs, hb0 + per);
+
+    fx16 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    // db: this thread's G rows are image rows 128 i + t/4 for i = 2, 3 (4 samples each)
+    float dbs[2] = {0.0f, 0.0f};
+
+    Loads L0, L1;
+    issue_loads(a, l, hb0, hb1, L0);
+    issue_loads(a, l, hb0 + 1, hb1, L1);
+    if (hb0 < hb1) {
+        dbs[0] += (L0.v[2][0] + L0.v[2][1]) + (L0.v[2][2] + L0.v[2][3]);
+        dbs[1] += (L0.v[3][0] + L0.v[3][1]) + (L0.v[3][2] + L0.v[3][3]);
+        write_planes(L0, lds);
+    }
+    __syncthreads();
+    if (active) hb_loop<true>(a, l, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds);
+    else hb_loop<false>(a, l, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds);
+
+    // partial [split][k][j], k < KT*32, j < NT*32 (32x32 C/D layout: row (r&3)+8(r>>2)+4h, col l&31)
+    if (active) {
+        const int ncol = NT * 32, h = lane >> 5;
+        float* part = a.dw_part + a.dwp_off[l] + (size_t)sp * (KT * 32) * ncol;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int kb = a0 + 32 * i, jb = g0 + 32 * j;
+                if (kb < KT * 32 && jb < ncol) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int k = kb + (r & 3) + 8 * (r >> 2) + 4 * h;
+                        part[(size_t)k * ncol + jb + (lane & 31)] = acc[i][j][r];
+                    }
+                }
+            }
+    }
+    // db: 4 threads per G row -> in-order sum through LDS
+    float* red = (float*)lds;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) red[(i * 128 + (tid >> 2)) * 4 + (tid & 3)] = dbs[i];
+    __syncthreads();
+    if (tid < NT * 32) {
+        const float* q = red + tid * 4;
+        a.db_part[a.dbp_off[l] + (size_t)sp * NT * 32 + tid] = (q[0] + q[1]) + (q[2] + q[3]);
+    }
+}
+
+}  // namespace
+
+void dw16_launch(const FusedPlan& p, hipStream_t s) {
+    Dw16Args a{};
+    for (int l = 0; l < p.L; ++l) {
+        a.kt[l] = p.kt[l];
+        a.nt[l] = p.nt[l];
+        a.a_off[l] = (l == 0) ? p.x_off : p.act_off[l - 1];
+        a.g_off[l] = p.grad_off[l];
+        a.splits[l] = p.dw_splits[l];
+        a.dwp_off[l] = p.dwp_off[l];
+        a.dbp_off[l] = p.dbp_off[l];
+        a.lid[l] = l;
+        a.wg_off[l] = p.dw_split_off[l];
+    }
+    a.wg_off[p.L] = p.dw_grid;
+    a.nl = p.L;
+    a.act = p.act;
+    a.grad = p.grad;
+    a.blocks = p.blocks;
+    a.dw_part = p.dw_part;
+    a.db_part = p.db_part;
+    dw16_kernel<<<p.dw_grid, kThreads, 0, s>>>(a);
+}
+
+}  // namespace lnerf

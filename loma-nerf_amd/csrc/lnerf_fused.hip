@@ -1695,6 +1695,11 @@ void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws
     // LNERF_K16=0 selects the one-wave-per-SIMD kernel (fused_fwd_bwd_kernel) for A/B runs
     const char* e = getenv("LNERF_K16");
     p.k16 = (e && e[0] == '0') ? 0 : (k16_supported(p) ? 1 : 0);
+    // dW: dw16_kernel for the bf16x6 split (LNERF_DW16=0: dw_all_kernel); one partial per split
+    const char* e2 = getenv("LNERF_DW16");
+    p.dw16 = (e2 && e2[0] == '0') ? 0 : (p.x6 == 3 ? 1 : 0);
+    if (p.dw16)
+        for (int l = 0; l < p.L; ++l) p.dw_phases[l] = 1;
 }
 
 static void launch_pack(const FusedPlan& p, const float* ws, const float* bs, hipStream_t s) {
@@ -1864,7 +1869,8 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
         da.wg_off[l] = p.dw_split_off[l];
     }
     da.wg_off[p.L] = p.dw_grid;
-    launch_dw_all(p.dw_grid, da, p.x6 != 0, s);
+    if (p.dw16) dw16_launch(p, s);
+    else launch_dw_all(p.dw_grid, da, p.x6 != 0, s);
     mark(4);
     ReduceArgs ra{};
     ra.L = p.L;

@@ -157,6 +157,7 @@ struct FusedPlan {
     size_t w16f_off[kMaxLayers], w16b_off[kMaxLayers];
     float* b16;                          // [L][256] zero-padded biases
     unsigned long long* mask_g;          // [num_wg][L-1][8 waves][64 lanes] ReLU mask bits
+    int dw16;                            // 1: dW by dw16_kernel (lnerf_dw16.hip), one partial per split
 };
 
 bool fused_supported(const lnerf_mlp& mlp, int rays, int S, int input_mode, const char** why);
@@ -171,6 +172,7 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
                       hipEvent_t* ev);
 void fused_render(const FusedPlan& p, const float* ws, const float* bs, const lnerf_batch& b,
                   const lnerf_outputs& out, hipStream_t s);
+void dw16_launch(const FusedPlan& p, hipStream_t s);
 // k16 kernel entry points (lnerf_k16.hip)
 bool k16_supported(const FusedPlan& p);
 void k16_pack(const FusedPlan& p, const float* ws, const float* bs, hipStream_t s);

@@ -168,7 +168,9 @@ def bench_render(args, world, rank, local, dist):
             "config": {"workload": "cfg5: 800x800 rays x 128 samples per frame, PE F=5, "
                                    "MLP 33->256x7->4, forward only",
                        "rays_per_gpu": N, "parallelism": f"replicas{world}"},
-            "roofline": {"bound": "mfma", "kernel": "fused_fwd_bwd_kernel (forward only)",
+            "roofline": {"bound": "mfma",
+                         "kernel": ("fused_fwd_bwd_kernel" if args.mfma_f32 else "k16_fwd_bwd_kernel") +
+                                   " (forward only)",
                          "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,
                          "traffic": None,
                          "note": "rank-0 per-GPU rate: 2*sum(KN) FLOP/sample x its samples / "
@@ -289,7 +291,11 @@ def main():
         if kt:
             fus_ms = kt["fused"]
             peak = PEAK_FP32_TFLOPS if args.mfma_f32 else PEAK_X6_TFLOPS
-            out["roofline"] = {"bound": "mfma", "kernel": "fused_fwd_bwd_kernel",
+            # the fused kernel the engine ran: k16 (wave pairs, default for the bf16 planes) or
+            # the one-wave-per-SIMD kernel (exact f32 MFMA, or LNERF_K16=0)
+            k1 = ("fused_fwd_bwd_kernel" if args.mfma_f32 or os.environ.get("LNERF_K16") == "0"
+                  else "k16_fwd_bwd_kernel")
+            out["roofline"] = {"bound": "mfma", "kernel": k1,
                                "achieved": fused_flops / (fus_ms / 1e3) / 1e12,
                                "peak": peak, "unit": "TFLOP/s",
                                "frac": fused_flops / (fus_ms / 1e3) / 1e12 / peak,
@@ -298,7 +304,7 @@ def main():
                                "peak_basis": ("f32 MFMA dense 157.3 TF" if args.mfma_f32 else
                                               "bf16 MFMA dense 2516.6 TF / 6 (bf16x6: six bf16 "
                                               "products per fp32-accurate multiply-add)")}
-            tr = pmc_traffic("fused_fwd_bwd_kernel", args.config) if args.rays is None else None
+            tr = pmc_traffic(k1, args.config) if args.rays is None else None
             if tr:
                 out["roofline"]["traffic"] = tr["bytes"]
                 out["roofline"]["traffic_unit"] = "bytes/launch"

@@ -58,19 +58,27 @@ struct Dw16Args {
 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
-// Address of the 16 B that thread t loads in round i (0..3) of half-block hb: image row
-// r = 128 i + t / 4 (A rows below 256, G rows from 256), samples 4 (t % 4) .. +3. A slab block
-// is [tile][half][32 rows][16 samples]; a half-block is one half of one 32-sample block.
-__device__ __forceinline__ const fx4* row_src(const Dw16Args& a, int l, int hb, int i, bool& ok) {
-    const int t = threadIdx.x, r = 128 * i + (t >> 2), q = t & 3;
-    const int blk = hb >> 1, half = hb & 1;
-    const bool isA = r < 256;
-    const int rr = isA ? r : r - 256;
-    const int tiles = isA ? a.kt[l] : a.nt[l];
-    ok = (rr >> 5) < tiles;
-    const int rc = ok ? rr : (rr & 31);   // a valid row of tile 0 when past the layer's tiles
-    const float* base = isA ? a.act + a.a_off[l] : a.grad + a.g_off[l];
-    return (const fx4*)(base + (size_t)blk * tiles * 1024 + (rc >> 5) * 1024 + half * 512 + (rc & 31) * 16 + 4 * q);
+// The 16 B that thread t loads in round i (0..3) of a half-block: image row r = 128 i + t / 4
+// (rounds 0, 1: A rows; 2, 3: G rows), samples 4 (t % 4) .. +3. A slab block is
+// [tile][half][32 rows][16 samples]; a half-block is one half of one 32-sample block. The
+// per-thread part of the offset is fixed (RowMap), the half-block part is wave-uniform.
+struct RowMap {
+    int off[4];      // float offset inside a half-block of the slab
+    bool ok[4];      // the row exists in this layer (else the value is zero)
+};
+
+__device__ __forceinline__ RowMap row_map(int kt, int nt) {
+    RowMap m;
+    const int t = threadIdx.x, q = t & 3;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int rr = 128 * (i & 1) + (t >> 2);   // row within A (i < 2) or G (i >= 2)
+        const int tiles = i < 2 ? kt : nt;
+        m.ok[i] = (rr >> 5) < tiles;
+        const int rc = m.ok[i] ? rr : (rr & 31);   // a valid row of tile 0 past the layer's tiles
+        m.off[i] = (rc >> 5) * 1024 + (rc & 31) * 16 + 4 * q;
+    }
+    return m;
 }
 
 struct Loads {
@@ -79,15 +87,18 @@ struct Loads {
 
 // Always four loads (rows past the layer's tiles and half-blocks past the split read a valid
 // address and are zeroed), so the compiler's vmcnt for them is exact.
-__device__ __forceinline__ void issue_loads(const Dw16Args& a, int l, int hb, int hb_end, Loads& L) {
+__device__ __forceinline__ void issue_loads(const float* A, const float* G, int kt, int nt, const RowMap& m,
+                                            int hb, int hb_end, Loads& L) {
     const bool in = hb < hb_end;
     const int hbc = in ? hb : max(0, hb_end - 1);
+    const int blk = hbc >> 1, half = hbc & 1;
+    const float* pa = A + (size_t)blk * kt * 1024 + half * 512;
+    const float* pg = G + (size_t)blk * nt * 1024 + half * 512;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        bool ok;
-        const fx4* p = row_src(a, l, hbc, i, ok);
+        const fx4* p = (const fx4*)((i < 2 ? pa : pg) + m.off[i]);
         const fx4 v = LNERF_DW16_NOLOAD ? fx4{1.0f, 2.0f, 3.0f, (float)i} : __builtin_nontemporal_load(p);
-        L.v[i] = (ok && in) ? v : fx4{0.0f, 0.0f, 0.0f, 0.0f};
+        L.v[i] = (m.ok[i] && in) ? v : fx4{0.0f, 0.0f, 0.0f, 0.0f};
     }
 }
 
@@ -165,13 +176,13 @@ __device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int 
 
 // The half-block loop of one split: L0 holds hb0 (already in the image), L1 hb0 + 1.
 template <bool ACTIVE>
-__device__ __forceinline__ void hb_loop(const Dw16Args& a, int l, int hb0, int hb1, int a0, int g0,
-                                        fx16 (&acc)[2][4], Loads& L0, Loads& L1, float (&dbs)[2],
-                                        unsigned char* lds) {
+__device__ __forceinline__ void hb_loop(const float* A, const float* G, int kt, int nt, const RowMap& m,
+                                        int hb0, int hb1, int a0, int g0, fx16 (&acc)[2][4], Loads& L0,
+                                        Loads& L1, float (&dbs)[2], unsigned char* lds) {
     for (int hb = hb0; hb < hb1; ++hb) {
         const int cur = (hb - hb0) & 1;
         // L1 holds hb + 1 (zeros past the end); L0 receives hb + 2
-        issue_loads(a, l, hb + 2, hb1, L0);
+        issue_loads(A, G, kt, nt, m, hb + 2, hb1, L0);
         dbs[0] += (L1.v[2][0] + L1.v[2][1]) + (L1.v[2][2] + L1.v[2][3]);
         dbs[1] += (L1.v[3][0] + L1.v[3][1]) + (L1.v[3][2] + L1.v[3][3]);
         block_mma<ACTIVE>(lds + cur * kImageBytes, a0, g0, acc, L1, lds + (cur ^ 1) * kImageBytes);
@@ -206,17 +217,20 @@ __global__ void __launch_bounds__(kThreads, 1) dw16_kernel(Dw16Args a) {
     // db: this thread's G rows are image rows 128 i + t/4 for i = 2, 3 (4 samples each)
     float dbs[2] = {0.0f, 0.0f};
 
+    const float* A = a.act + a.a_off[l];
+    const float* G = a.grad + a.g_off[l];
+    const RowMap m = row_map(KT, NT);
     Loads L0, L1;
-    issue_loads(a, l, hb0, hb1, L0);
-    issue_loads(a, l, hb0 + 1, hb1, L1);
+    issue_loads(A, G, KT, NT, m, hb0, hb1, L0);
+    issue_loads(A, G, KT, NT, m, hb0 + 1, hb1, L1);
     if (hb0 < hb1) {
         dbs[0] += (L0.v[2][0] + L0.v[2][1]) + (L0.v[2][2] + L0.v[2][3]);
         dbs[1] += (L0.v[3][0] + L0.v[3][1]) + (L0.v[3][2] + L0.v[3][3]);
         write_planes(L0, lds);
     }
     __syncthreads();
-    if (active) hb_loop<true>(a, l, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds);
-    else hb_loop<false>(a, l, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds);
+    if (active) hb_loop<true>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds);
+    else hb_loop<false>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds);
 
     // partial [split][k][j], k < KT*32, j < NT*32 (32x32 C/D layout: row (r&3)+8(r>>2)+4h, col l&31)
     if (active) {

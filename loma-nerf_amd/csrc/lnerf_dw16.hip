@@ -136,48 +136,51 @@ __device__ __forceinline__ fx16 mfma32(const bf8& a, const bf8& b, fx16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
-// The wave's 2 x 4 tile block on one half-block image (per 32-row tile a fragment is one
-// ds_read_b128 per plane; lane: row l & 31, samples 8 (l >> 5) .. +7), with the split of the
-// next half-block interleaved: round j of it beside output column tile j, so the VALU split
-// issues under the MFMAs. Branch-free (ACTIVE is a template parameter; past the split's last
-// half-block the zeroed loads land in the idle image buffer) so the scheduler can overlap it.
-template <bool ACTIVE>
-__device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int g0, fx16 (&acc)[2][4],
+// The wave's TI x TJ tile block (TI 32-row tiles of A, TJ of G) on one half-block image (per
+// tile a fragment is one ds_read_b128 per plane; lane: row l & 31, samples 8 (l >> 5) .. +7),
+// with the split of the next half-block interleaved (round k beside output column tile k), so
+// the VALU split issues under the MFMAs. Branch-free (ACTIVE is a template parameter; past the
+// split's last half-block the zeroed loads land in the idle image buffer).
+template <int TI, int TJ, bool ACTIVE>
+__device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int g0, fx16 (&acc)[TI][TJ],
                                           const Loads& nl, unsigned char* nxt) {
     const int lane = threadIdx.x & 63, fo = (lane & 31) * 32 + (lane >> 5) * 16;
-    bf8 ap[2][3];
+    bf8 ap[TI][3];
     if constexpr (ACTIVE) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
             for (int p = 0; p < 3; ++p) ap[i][p] = *(const bf8*)(img + p * kPlaneBytes + (a0 + 32 * i) * 32 + fo);
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        write_planes_row(nl.v[j], j, nxt);
+    for (int k = 0; k < 4; ++k) {
+        write_planes_row(nl.v[k], k, nxt);
         if constexpr (ACTIVE) {
-            bf8 gp[3];
+            if (k < TJ) {
+                const int j = k < TJ ? k : 0;
+                bf8 gp[3];
 #pragma unroll
-            for (int p = 0; p < 3; ++p) gp[p] = *(const bf8*)(img + p * kPlaneBytes + (256 + g0 + 32 * j) * 32 + fo);
+                for (int p = 0; p < 3; ++p) gp[p] = *(const bf8*)(img + p * kPlaneBytes + (256 + g0 + 32 * j) * 32 + fo);
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                fx16 c = acc[i][j];
-                c = mfma32(ap[i][0], gp[2], c);   // small terms first
-                c = mfma32(ap[i][1], gp[1], c);
-                c = mfma32(ap[i][2], gp[0], c);
-                c = mfma32(ap[i][1], gp[0], c);
-                c = mfma32(ap[i][0], gp[1], c);
-                c = mfma32(ap[i][0], gp[0], c);
-                acc[i][j] = c;
+                for (int i = 0; i < TI; ++i) {
+                    fx16 c = acc[i][j];
+                    c = mfma32(ap[i][0], gp[2], c);   // small terms first
+                    c = mfma32(ap[i][1], gp[1], c);
+                    c = mfma32(ap[i][2], gp[0], c);
+                    c = mfma32(ap[i][1], gp[0], c);
+                    c = mfma32(ap[i][0], gp[1], c);
+                    c = mfma32(ap[i][0], gp[0], c);
+                    acc[i][j] = c;
+                }
             }
         }
     }
 }
 
 // The half-block loop of one split: L0 holds hb0 (already in the image), L1 hb0 + 1.
-template <bool ACTIVE>
+template <int TI, int TJ, bool ACTIVE>
 __device__ __forceinline__ void hb_loop(const float* A, const float* G, int kt, int nt, const RowMap& m,
-                                        int hb0, int hb1, int a0, int g0, fx16 (&acc)[2][4], Loads& L0,
+                                        int hb0, int hb1, int a0, int g0, fx16 (&acc)[TI][TJ], Loads& L0,
                                         Loads& L1, float (&dbs)[2], unsigned char* lds) {
     for (int hb = hb0; hb < hb1; ++hb) {
         const int cur = (hb - hb0) & 1;
@@ -185,7 +188,7 @@ __device__ __forceinline__ void hb_loop(const float* A, const float* G, int kt, 
         issue_loads(A, G, kt, nt, m, hb + 2, hb1, L0);
         dbs[0] += (L1.v[2][0] + L1.v[2][1]) + (L1.v[2][2] + L1.v[2][3]);
         dbs[1] += (L1.v[3][0] + L1.v[3][1]) + (L1.v[3][2] + L1.v[3][3]);
-        block_mma<ACTIVE>(lds + cur * kImageBytes, a0, g0, acc, L1, lds + (cur ^ 1) * kImageBytes);
+        block_mma<TI, TJ, ACTIVE>(lds + cur * kImageBytes, a0, g0, acc, L1, lds + (cur ^ 1) * kImageBytes);
         __syncthreads();
         Loads t = L0;
         L0 = L1;
@@ -193,27 +196,25 @@ __device__ __forceinline__ void hb_loop(const float* A, const float* G, int kt, 
     }
 }
 
-__global__ void __launch_bounds__(kThreads, 1) dw16_kernel(Dw16Args a) {
-    __shared__ __attribute__((aligned(16))) unsigned char lds[kLdsBytes];
-    int li = 0;
-    while (li + 1 < a.nl && (int)blockIdx.x >= a.wg_off[li + 1]) ++li;
-    const int l = a.lid[li], sp = blockIdx.x - a.wg_off[li];
+// One split of layer l with TI x TJ tile blocks per wave (the layer's ceil(KT/TI) x ceil(NT/TJ)
+// blocks on waves 0.., at most 8).
+template <int TI, int TJ>
+__device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsigned char* lds) {
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
     const int KT = a.kt[l], NT = a.nt[l];
-    // wave block: in rows [a0, a0 + 64), out rows [g0, g0 + 128)
-    const int nbg = (NT + 3) >> 2, nblk = ((KT + 1) >> 1) * nbg;
+    const int nbg = (NT + TJ - 1) / TJ, nblk = ((KT + TI - 1) / TI) * nbg;
     const bool active = wave < nblk && !LNERF_DW16_NOMMA;
-    const int a0 = active ? (wave / nbg) * 64 : 0, g0 = active ? (wave % nbg) * 128 : 0;
+    const int a0 = active ? (wave / nbg) * 32 * TI : 0, g0 = active ? (wave % nbg) * 32 * TJ : 0;
     // half-block range of this split
     const int hbs = 2 * a.blocks, splits = a.splits[l];
     const int per = (hbs + splits - 1) / splits;
     const int hb0 = min(hbs, sp * per), hb1 = min(hbs, hb0 + per);
 
-    fx16 acc[2][4];
+    fx16 acc[TI][TJ];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (int j = 0; j < TJ; ++j) acc[i][j] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     // db: this thread's G rows are image rows 128 i + t/4 for i = 2, 3 (4 samples each)
     float dbs[2] = {0.0f, 0.0f};
 
@@ -229,17 +230,17 @@ __global__ void __launch_bounds__(kThreads, 1) dw16_kernel(Dw16Args a) {
         write_planes(L0, lds);
     }
     __syncthreads();
-    if (active) hb_loop<true>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds);
-    else hb_loop<false>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds);
+    if (active) hb_loop<TI, TJ, true>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds);
+    else hb_loop<TI, TJ, false>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds);
 
     // partial [split][k][j], k < KT*32, j < NT*32 (32x32 C/D layout: row (r&3)+8(r>>2)+4h, col l&31)
     if (active) {
         const int ncol = NT * 32, h = lane >> 5;
         float* part = a.dw_part + a.dwp_off[l] + (size_t)sp * (KT * 32) * ncol;
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < TJ; ++j) {
                 const int kb = a0 + 32 * i, jb = g0 + 32 * j;
                 if (kb < KT * 32 && jb < ncol) {
 #pragma unroll
@@ -258,6 +259,26 @@ __global__ void __launch_bounds__(kThreads, 1) dw16_kernel(Dw16Args a) {
     if (tid < NT * 32) {
         const float* q = red + tid * 4;
         a.db_part[a.dbp_off[l] + (size_t)sp * NT * 32 + tid] = (q[0] + q[1]) + (q[2] + q[3]);
+    }
+}
+
+// Block shape per layer: the smallest of 1x1, 1x2, 2x4 tiles that needs at most 8 waves, so
+// small layers (the head, layer 0) spread over all SIMDs instead of a few waves.
+__host__ __device__ __forceinline__ int dw_shape(int kt, int nt) {
+    if (kt * nt <= 8) return 0;
+    if (kt * ((nt + 1) / 2) <= 8) return 1;
+    return 2;
+}
+
+__global__ void __launch_bounds__(kThreads, 1) dw16_kernel(Dw16Args a) {
+    __shared__ __attribute__((aligned(16))) unsigned char lds[kLdsBytes];
+    int li = 0;
+    while (li + 1 < a.nl && (int)blockIdx.x >= a.wg_off[li + 1]) ++li;
+    const int l = a.lid[li], sp = blockIdx.x - a.wg_off[li];
+    switch (dw_shape(a.kt[l], a.nt[l])) {
+        case 0: dw_split<1, 1>(a, l, sp, lds); break;
+        case 1: dw_split<1, 2>(a, l, sp, lds); break;
+        default: dw_split<2, 4>(a, l, sp, lds); break;
     }
 }
 

@@ -104,7 +104,7 @@ __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane
 #define LNERF_PROF 0
 #endif
 #if LNERF_PROF
-enum { kPfPE, kPfFwd, kPfFwdEpi, kPfBar, kPfComp, kPfBwd, kPfBwdEpi, kPfTail, kPfTotal, kPfVm, kPfN };
+enum { kPfPE, kPfFwd, kPfFwdEpi, kPfBar, kPfComp, kPfBwd, kPfBwdEpi, kPfTail, kPfTotal, kPfVm, kPfReal, kPfN };
 __device__ unsigned long long g_k16_prof[16];
 __device__ __forceinline__ unsigned long long* prof_slots() {
     __shared__ unsigned long long sl[kWaves][16];
@@ -308,6 +308,8 @@ __device__ __forceinline__ void k16_pass(const K16Args& a, int ks, int& ci, unsi
             bf8 w[kDist + 1][3];
             read_tile<PL, 0>(base, w[0]);
             if constexpr (NTO > 1) read_tile<PL, 1>(base, w[1]);
+            // (an LDS-transposed form -- 8 ds_write_b32 + 2 ds_read_b128 + 2 dwordx4 stores --
+            // measured slower: 2.13-2.18 vs 2.02-2.03 ms)
             if (slab && !LNERF_K16_NOSTORE) store_slab_step(slab + s * 1024, in[2 * s], in[2 * s + 1]);
             bf8 bh, bm = {}, bl = {};
 #pragma unroll
@@ -391,6 +393,7 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
 #if LNERF_PROF
     if (lane < 16) prof_slots()[lane] = 0;
     PROF_T(t_start);
+    const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
 #endif
 
     fx4 act[kMaxT], out[kMaxT];
@@ -552,6 +555,7 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
 #if LNERF_PROF
     PROF_ADD(kPfTail, t_t);
     PROF_ADD(kPfTotal, t_start);
+    if (lane == 0) prof_slots()[kPfReal] += __builtin_amdgcn_s_memrealtime() - rt_start;
     if (lane < kPfN) atomicAdd(&g_k16_prof[lane], prof_slots()[lane]);
 #endif
 }
@@ -714,10 +718,10 @@ void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lner
         (void)hipStreamSynchronize(s);
         (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_k16_prof), sizeof(h));
         const char* names[] = {"pe", "fwd_pass", "fwd_epilogue", "barrier", "composite", "bwd_pass",
-                               "bwd_epilogue", "tail", "total", "vmcnt_wait"};
+                               "bwd_epilogue", "tail", "total", "vmcnt_wait", "realtime_100MHz"};
         fprintf(stderr, "LNERF_PROF k16 per-wave cycles:");
         for (int i = 0; i < kPfN; ++i) fprintf(stderr, " %s=%.0f", names[i], h[i] / ((double)p.num_wg * kWaves));
-        fprintf(stderr, "\n");
+        fprintf(stderr, " clock_GHz=%.3f\n", h[kPfReal] ? (double)h[kPfTotal] / h[kPfReal] * 0.1 : 0.0);
         unsigned long long z[16] = {};
         (void)hipMemcpyToSymbol(HIP_SYMBOL(g_k16_prof), z, sizeof(z));
     }

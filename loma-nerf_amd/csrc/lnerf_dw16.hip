@@ -141,9 +141,9 @@ __device__ __forceinline__ fx16 mfma32(const bf8& a, const bf8& b, fx16 c) {
 // with the split of the next half-block interleaved (round k beside output column tile k), so
 // the VALU split issues under the MFMAs. Branch-free (ACTIVE is a template parameter; past the
 // split's last half-block the zeroed loads land in the idle image buffer).
-template <int TI, int TJ, bool ACTIVE>
+template <int TI, int TJ, bool ACTIVE, bool FULL>
 __device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int g0, fx16 (&acc)[TI][TJ],
-                                          const Loads& nl, unsigned char* nxt) {
+                                          const Loads& nl, unsigned char* nxt, const RowMap& m) {
     const int lane = threadIdx.x & 63, fo = (lane & 31) * 32 + (lane >> 5) * 16;
     bf8 ap[TI][3];
     if constexpr (ACTIVE) {
@@ -154,7 +154,9 @@ __device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int 
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        write_planes_row(nl.v[k], k, nxt);
+        // rows past the layer's tiles are never read: skip their split (wave-uniform: a wave's
+        // 16 rows of a round lie in one 32-row tile); FULL layers need no branch
+        if (FULL || m.ok[k]) write_planes_row(nl.v[k], k, nxt);
         if constexpr (ACTIVE) {
             if (k < TJ) {
                 const int j = k < TJ ? k : 0;
@@ -178,7 +180,7 @@ __device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int 
 }
 
 // The half-block loop of one split: L0 holds hb0 (already in the image), L1 hb0 + 1.
-template <int TI, int TJ, bool ACTIVE>
+template <int TI, int TJ, bool ACTIVE, bool FULL>
 __device__ __forceinline__ void hb_loop(const float* A, const float* G, int kt, int nt, const RowMap& m,
                                         int hb0, int hb1, int a0, int g0, fx16 (&acc)[TI][TJ], Loads& L0,
                                         Loads& L1, float (&dbs)[2], unsigned char* lds) {
@@ -188,7 +190,7 @@ __device__ __forceinline__ void hb_loop(const float* A, const float* G, int kt, 
         issue_loads(A, G, kt, nt, m, hb + 2, hb1, L0);
         dbs[0] += (L1.v[2][0] + L1.v[2][1]) + (L1.v[2][2] + L1.v[2][3]);
         dbs[1] += (L1.v[3][0] + L1.v[3][1]) + (L1.v[3][2] + L1.v[3][3]);
-        block_mma<TI, TJ, ACTIVE>(lds + cur * kImageBytes, a0, g0, acc, L1, lds + (cur ^ 1) * kImageBytes);
+        block_mma<TI, TJ, ACTIVE, FULL>(lds + cur * kImageBytes, a0, g0, acc, L1, lds + (cur ^ 1) * kImageBytes, m);
         __syncthreads();
         Loads t = L0;
         L0 = L1;
@@ -230,8 +232,11 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
         write_planes(L0, lds);
     }
     __syncthreads();
-    if (active) hb_loop<TI, TJ, true>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds);
-    else hb_loop<TI, TJ, false>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds);
+    const bool full = KT == 8 && NT == 8;
+    if (active && full) hb_loop<TI, TJ, true, true>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds);
+    else if (active) hb_loop<TI, TJ, true, false>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds);
+    else if (full) hb_loop<TI, TJ, false, true>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds);
+    else hb_loop<TI, TJ, false, false>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds);
 
     // partial [split][k][j], k < KT*32, j < NT*32 (32x32 C/D layout: row (r&3)+8(r>>2)+4h, col l&31)
     if (active) {

@@ -1,8 +1,12 @@
 #!/usr/bin/env python3
 """Accuracy of each step implementation against the float64 numpy restatement (oracle/nerf_np.py)
 on a cfg3 subset (the bench MLP 33->256x7->4, 64 samples): the C loma-order fp32 oracle, the
-generic device path, the fused path with exact f32 MFMA and with the bf16x6 split. Test/report
-infrastructure (imports the oracle); writes gpurun_out/precision.json.
+generic device path, the fused path with exact f32 MFMA, with the bf16x6 split (k16 + dw16, the
+default) and the one-wave-per-SIMD bf16x6 kernel (LNERF_K16=0). Reported twice: on all rays, and
+without the rays holding a ReLU decision below fp32 resolution (nerf_np.relu_tie_rays: |z| <
+5e-7 sum|terms|, where any fp32 summation order may decide either way and the flipped sample's
+whole gradient row moves). Test/report infrastructure (imports the oracle); writes
+gpurun_out/precision.json.
 
     python scripts/precision_report.py [--rays 64]
 """
@@ -33,44 +37,61 @@ def errors(got, ref):
     return out
 
 
+def f64_reference(w):
+    import nerf_np
+    X64 = nerf_np.positional_encoding_3d(w.pts32.astype(np.float64), w.F).reshape(w.X.shape)
+    ref = nerf_np.nerf_forward_backward(X64, [x.astype(np.float64) for x in w.ws],
+                                        [x.astype(np.float64) for x in w.bs], w.dists, w.target,
+                                        w.S, seed=1.0)
+    dW = np.zeros(w.wp.shape)
+    dB = np.zeros(w.bp.shape)
+    for l in range(len(w.ws)):
+        k, n = w.ws[l].shape
+        dW[l, :k, :n] = ref["dW"][l]
+        dB[l, :n] = ref["db"][l]
+    return dict(loss=ref["loss"], acc=ref["acc"], dW=dW, dB=dB, d_dists=ref["d_dists"],
+                d_target=ref["d_target"])
+
+
+def report(eng, w):
+    import lnerf
+    from test_gpu_native import oracle_ref, run_native
+    ref = f64_reference(w)
+    rep = {"oracle_c_fp32": errors(oracle_ref(w, seed=1.0), ref),
+           "generic_device": errors(run_native(eng, w, seed=1.0, flags=lnerf.GENERIC), ref),
+           "fused_f32_mfma": errors(run_native(eng, w, seed=1.0, flags=lnerf.FAST | lnerf.MFMA_F32), ref),
+           "fused_bf16x6_k16_dw16": errors(run_native(eng, w, seed=1.0, flags=lnerf.FAST), ref)}
+    os.environ["LNERF_K16"] = "0"
+    os.environ["LNERF_DW16"] = "0"
+    rep["fused_bf16x6_one_wave_kernels"] = errors(run_native(eng, w, seed=1.0, flags=lnerf.FAST), ref)
+    del os.environ["LNERF_K16"]
+    del os.environ["LNERF_DW16"]
+    return rep
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rays", type=int, default=64)
     args = ap.parse_args()
     import lnerf
     import nerf_np
-    import oracle
-    from test_gpu_native import oracle_ref, run_native
 
     w = nerf_np.make_workload("cfg3", rays=args.rays)
-    X64 = nerf_np.positional_encoding_3d(w.pts32.astype(np.float64), w.F).reshape(w.X.shape)
-    ref = nerf_np.nerf_forward_backward(X64, [x.astype(np.float64) for x in w.ws],
-                                        [x.astype(np.float64) for x in w.bs], w.dists, w.target,
-                                        w.S, seed=1.0)
-    L = len(w.ws)
-    dW = np.zeros(w.wp.shape)
-    dB = np.zeros(w.bp.shape)
-    for l in range(L):
-        k, n = w.ws[l].shape
-        dW[l, :k, :n] = ref["dW"][l]
-        dB[l, :n] = ref["db"][l]
-    ref = dict(loss=ref["loss"], acc=ref["acc"], dW=dW, dB=dB, d_dists=ref["d_dists"],
-               d_target=ref["d_target"])
-
+    ties = nerf_np.relu_tie_rays(w)
     eng = lnerf.Engine(0)
     rep = {"workload": f"cfg3 subset: {args.rays} rays x {w.S} samples, MLP 33->256x7->4, seed 1",
-           "reference": "float64 numpy restatement (oracle/nerf_np.py)"}
-    rep["oracle_c_fp32"] = errors(oracle_ref(w, seed=1.0), ref)
-    rep["generic_device"] = errors(run_native(eng, w, seed=1.0, flags=lnerf.GENERIC), ref)
-    rep["fused_f32_mfma"] = errors(run_native(eng, w, seed=1.0, flags=lnerf.FAST | lnerf.MFMA_F32), ref)
-    rep["fused_bf16x6"] = errors(run_native(eng, w, seed=1.0, flags=lnerf.FAST), ref)
+           "reference": "float64 numpy restatement (oracle/nerf_np.py)",
+           "all_rays": report(eng, w),
+           "tie_rays": [int(r) for r in ties],
+           "without_tie_rays": report(eng, nerf_np.without_relu_ties(w))}
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
     with open(os.path.join(REPO, "gpurun_out", "precision.json"), "w") as fh:
         json.dump(rep, fh, indent=1)
-    for k, v in rep.items():
-        if isinstance(v, dict):
-            print(k, {kk: (vv["max_abs_over_max"] if isinstance(vv, dict) else vv)
-                      for kk, vv in v.items()})
+    for part in ("all_rays", "without_tie_rays"):
+        print(part)
+        for k, v in rep[part].items():
+            print(" ", k, {kk: (float("%.3g" % vv["max_abs_over_max"]) if isinstance(vv, dict) else vv)
+                           for kk, vv in v.items()})
     eng.close()
 
 

@@ -243,7 +243,18 @@ __device__ __forceinline__ void lgkm_wait(bf8 (&w)[3]) {
     asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]) : "n"(N));
 }
 
-constexpr int kDist = 2;   // weight tiles read ahead of the one the MFMAs consume
+template <int N>
+__device__ __forceinline__ void lgkm_wait1(bf8& w) {
+    asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(w) : "n"(N));
+}
+
+#ifndef LNERF_K16_DIST
+#define LNERF_K16_DIST 2
+#endif
+constexpr int kDist = LNERF_K16_DIST;   // weight tiles read ahead of the one the MFMAs consume
+#ifndef LNERF_K16_FINEWAIT
+#define LNERF_K16_FINEWAIT 0           // 1: per-plane lgkmcnt waits inside a tile's MFMAs
+#endif
 
 template <int PL, int O>
 __device__ __forceinline__ void read_tile(unsigned base, bf8 (&w)[3]) {
@@ -262,11 +273,14 @@ __device__ __forceinline__ void tile_step(unsigned base, bf8 (&w)[kDist + 1][3],
     if constexpr (O + kDist < NTO) read_tile<PL, O + kDist>(base, w[(O + kDist) % (kDist + 1)]);
     constexpr int ahead = (NTO - 1 - O) < kDist ? (NTO - 1 - O) : kDist;
     bf8(&c)[3] = w[O % (kDist + 1)];
-    lgkm_wait<ahead * PL>(c);
+    if constexpr (LNERF_K16_FINEWAIT && PL == 3) lgkm_wait1<ahead * PL + 2>(c[0]);
+    else lgkm_wait<ahead * PL>(c);
     fx4 acc = out[O];
     if constexpr (PL == 3) {
         acc = mfma16(c[0], bl, acc);
+        if constexpr (LNERF_K16_FINEWAIT) lgkm_wait1<ahead * PL + 1>(c[1]);
         acc = mfma16(c[1], bm, acc);
+        if constexpr (LNERF_K16_FINEWAIT) lgkm_wait1<ahead * PL>(c[2]);
         acc = mfma16(c[2], bh, acc);
         acc = mfma16(c[1], bh, acc);
         acc = mfma16(c[0], bm, acc);
@@ -308,6 +322,7 @@ __device__ __forceinline__ void k16_pass(const K16Args& a, int ks, int& ci, unsi
             bf8 w[kDist + 1][3];
             read_tile<PL, 0>(base, w[0]);
             if constexpr (NTO > 1) read_tile<PL, 1>(base, w[1]);
+            if constexpr (kDist > 2 && NTO > 2) read_tile<PL, 2>(base, w[2]);
             // (an LDS-transposed form -- 8 ds_write_b32 + 2 ds_read_b128 + 2 dwordx4 stores --
             // measured slower: 2.13-2.18 vs 2.02-2.03 ms)
             if (slab && !LNERF_K16_NOSTORE) store_slab_step(slab + s * 1024, in[2 * s], in[2 * s + 1]);
@@ -325,7 +340,7 @@ __device__ __forceinline__ void k16_pass(const K16Args& a, int ks, int& ci, unsi
                     bh[j] = (__bf16)x;
                 }
             }
-            static_assert(kDist == 2, "prologue reads two tiles");
+            static_assert(kDist == 2 || kDist == 3, "the prologue reads kDist tiles");
             tile_steps<NTO, PL>(std::make_integer_sequence<int, NTO>{}, base, w, bh, bm, bl, out);
             dma_barrier(pending);
             ++ci;

@@ -103,6 +103,26 @@ def test_fused_nonuniform_widths(engine, prec):
     compare(got, want)
 
 
+def test_fused_deep_mlp(engine):
+    """12 layers (33->64x11->4): the k16 kernel's chunk stream (2 passes x 11 hidden layers) and
+    its HBM ReLU masks beyond the 8 hidden layers the one-wave kernel keeps in LDS."""
+    w = nerf_np.make_workload("cfg2", rays=32, samples=32)
+    rng = np.random.RandomState(7)
+    dims = [33] + [64] * 11 + [4]
+    ws = [(rng.randn(k, n) * np.sqrt(2.0 / k)).astype(np.float32) for k, n in zip(dims, dims[1:])]
+    bs = [(rng.randn(n) * 0.5).astype(np.float32) for n in dims[1:]]
+    wp = np.zeros((len(ws), 64, 64), np.float32)
+    bp = np.zeros((len(ws), 64), np.float32)
+    for l, (a, b) in enumerate(zip(ws, bs)):
+        wp[l, :a.shape[0], :a.shape[1]] = a
+        bp[l, :b.shape[0]] = b
+    w = nerf_np.Workload(w.pts, w.pts32, w.X, w.dists, w.target, ws, bs, wp, bp, w.F, w.S, w.N)
+    w = nerf_np.without_relu_ties(w)
+    got = run_native(engine, w)
+    want = oracle_ref(w)
+    compare(got, want)
+
+
 def test_fused_ragged_rays_and_samples(engine):
     """S that does not divide the 128-sample tile (30, as train_nerf.py uses), a ray count that
     leaves a partial workgroup, and S = 1 / S = 128 edges."""

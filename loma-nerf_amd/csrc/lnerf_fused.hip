@@ -1550,7 +1550,9 @@ void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S, bool train = tr
     // layers in proportion to the slab bytes each one streams (kt + nt tiles per 32-sample
     // block): the kernel is bandwidth-bound, so equal bytes per workgroup balance it. Phased
     // (small) layers write 4 partials per split.
-    constexpr int kDwGrid = 512;
+    // (LNERF_DW_GRID overrides the workgroup budget for A/B runs)
+    const char* eg = getenv("LNERF_DW_GRID");
+    const int kDwGrid = eg ? atoi(eg) : 512;
     size_t dwp = 0, dbp = 0;
     int tiles_sum = 0;
     for (int l = 0; l < L; ++l) {

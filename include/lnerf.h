@@ -179,6 +179,18 @@ int lnerf_render(lnerf_ctx* ctx, const lnerf_mlp* mlp, const float* ws, const fl
  * of values written (0 if no timed step ran on the fused path). */
 int lnerf_ctx_timings(lnerf_ctx* ctx, float* ms_out, int n);
 
+/* Which kernels the last lnerf_train_step / lnerf_render on `ctx` ran (for tests and benches):
+ * a mask of LNERF_PATH_* bits, the bf16 planes per operand of the fused MFMAs in bits 8-9
+ * (3 = bf16x6 split, 1 = plain bf16, 0 = exact f32 or the generic path), or a negative error
+ * code. 0 if no step has run. */
+enum {
+    LNERF_PATH_GENERIC = 1,   /* the loma-order stage-by-stage kernels                        */
+    LNERF_PATH_FUSED = 2,     /* the fused MFMA step (any kernel pair below)                  */
+    LNERF_PATH_K16 = 4,       /* fused kernel on wave pairs (k16_fwd_bwd_kernel)              */
+    LNERF_PATH_DW16 = 8       /* dW kernel on wave pairs (dw16_kernel)                        */
+};
+int lnerf_ctx_last_path(lnerf_ctx* ctx);
+
 /* buf[i] *= *scale for i < n (device pointers): applies a loss seed after an all-reduce of
  * unit-seeded gradients (the data-parallel path). */
 int lnerf_scale_by_device_scalar(float* buf, size_t n, const float* scale, void* stream);

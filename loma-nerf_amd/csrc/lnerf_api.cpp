@@ -588,7 +588,13 @@ struct lnerf_ctx {
     std::mutex mu;
     hipEvent_t ev[7] = {};
     bool timed = false;
+    int last_path = 0;   // lnerf_ctx_last_path
 };
+
+static int path_bits(const FusedPlan& p, bool train) {
+    return LNERF_PATH_FUSED | (p.k16 ? LNERF_PATH_K16 : 0) | (train && p.dw16 ? LNERF_PATH_DW16 : 0) |
+           (p.x6 << 8);
+}
 
 extern "C" const char* lnerf_last_error(void) { return g_last_error.c_str(); }
 extern "C" const char* lnerf_version(void) { return "loma-nerf-amd 0.1 (gfx950)"; }
@@ -779,9 +785,11 @@ extern "C" int lnerf_train_step(lnerf_ctx* ctx, const lnerf_mlp* mlp, const floa
             const bool timed = (flags & LNERF_TIMING) != 0;
             fused_train_step(p, ws, bs, *batch, seed, flags, o, s, timed ? ctx->ev : nullptr);
             ctx->timed = timed;
+            ctx->last_path = path_bits(p, true);
         } else {
             generic_step(ctx, *mlp, ws, bs, *batch, seed, flags, o, true, s);
             ctx->timed = false;
+            ctx->last_path = LNERF_PATH_GENERIC;
         }
         check_launch("lnerf_train_step");
     });
@@ -811,8 +819,10 @@ extern "C" int lnerf_render(lnerf_ctx* ctx, const lnerf_mlp* mlp, const float* w
             FusedPlan p{};
             fused_plan(p, *mlp, *batch, ctx->fused_ws.get(bytes), flags, false);
             fused_render(p, ws, bs, *batch, o, s);
+            ctx->last_path = path_bits(p, false);
         } else {
             generic_step(ctx, *mlp, ws, bs, *batch, 1.0f, 0, o, false, s);
+            ctx->last_path = LNERF_PATH_GENERIC;
         }
         check_launch("lnerf_render");
     });
@@ -830,6 +840,16 @@ extern "C" int lnerf_ctx_timings(lnerf_ctx* ctx, float* ms_out, int n) {
         for (int i = 0; i < 6 && i < n; ++i) ms_out[written++] = v[i];
     });
     return rc != 0 ? rc : written;
+}
+
+extern "C" int lnerf_ctx_last_path(lnerf_ctx* ctx) {
+    int path = 0;
+    const int rc = guard_int([&]() {
+        if (!ctx) fail("null ctx");
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        path = ctx->last_path;
+    });
+    return rc != 0 ? rc : path;
 }
 
 extern "C" int lnerf_scale_by_device_scalar(float* buf, size_t n, const float* scale, void* stream) {

@@ -1550,9 +1550,15 @@ void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S, bool train = tr
     // layers in proportion to the slab bytes each one streams (kt + nt tiles per 32-sample
     // block): the kernel is bandwidth-bound, so equal bytes per workgroup balance it. Phased
     // (small) layers write 4 partials per split.
-    // (LNERF_DW_GRID overrides the workgroup budget for A/B runs)
-    const char* eg = getenv("LNERF_DW_GRID");
-    const int kDwGrid = eg ? atoi(eg) : 512;
+    // (LNERF_DW_GRID overrides the workgroup budget for A/B runs: read once, clamped to
+    // [16, 4096]; an unparsable value keeps the default)
+    static const int kDwGrid = [] {
+        const char* eg = getenv("LNERF_DW_GRID");
+        char* end = nullptr;
+        const long v = eg ? strtol(eg, &end, 10) : 0;
+        if (!eg || end == eg || *end != '\0') return 512;
+        return (int)(v < 16 ? 16 : v > 4096 ? 4096 : v);
+    }();
     size_t dwp = 0, dbp = 0;
     int tiles_sum = 0;
     for (int l = 0; l < L; ++l) {
@@ -1617,9 +1623,13 @@ void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws
     make_layout(y, m, b.rays, b.samples, train);
     p.L = m.num_layers;
     p.ht = y.ht;
-    // bf16x6 keeps (L-1)*HT ReLU-mask tiles in a smaller LDS budget (the ring is 1.5x larger)
-    // per-lane ReLU masks take 1 KiB per hidden layer and wave: (L-1) <= kMaskTiles / 8
-    const bool bf_ok = (p.L - 1) <= kMaskTiles(true) / 8;
+    // The bf16 planes run on k16 (ReLU masks in HBM, any depth) unless LNERF_K16=0 or the head
+    // is wider than one 16-wide tile; only the one-wave kernel keeps its masks in LDS, 1 KiB per
+    // hidden layer and wave in the bf16x6 budget: (L-1) <= kMaskTiles / 8. Past that depth the
+    // one-wave kernel falls back to exact f32 products.
+    const char* e = getenv("LNERF_K16");
+    const bool k16_wanted = !(e && e[0] == '0') && !(flags & LNERF_MFMA_F32) && m.n[p.L - 1] <= 16;
+    const bool bf_ok = k16_wanted || (p.L - 1) <= kMaskTiles(true) / 8;
     p.x6 = (flags & LNERF_MFMA_F32) || !bf_ok ? 0 : (flags & LNERF_MFMA_BF16) ? 1 : 3;
     for (int l = 0; l < p.L; ++l) {
         p.fo[l] = y.fo[l];
@@ -1695,8 +1705,8 @@ void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws
         p.w16b_off[l] = y.w16b_off[l];
     }
     // LNERF_K16=0 selects the one-wave-per-SIMD kernel (fused_fwd_bwd_kernel) for A/B runs
-    const char* e = getenv("LNERF_K16");
-    p.k16 = (e && e[0] == '0') ? 0 : (k16_supported(p) ? 1 : 0);
+    // (k16_wanted implies k16_supported: x6 is 1 or 3 and the head fits one tile)
+    p.k16 = k16_wanted && k16_supported(p) ? 1 : 0;
     // dW: dw16_kernel for the bf16x6 split (LNERF_DW16=0: dw_all_kernel); one partial per split
     const char* e2 = getenv("LNERF_DW16");
     p.dw16 = (e2 && e2[0] == '0') ? 0 : (p.x6 == 3 ? 1 : 0);

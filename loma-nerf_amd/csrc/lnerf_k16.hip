@@ -10,8 +10,8 @@
 //    = features 4(l >> 4) + i of each 16-feature tile), which is the next layer's B operand after
 //    a fixed permutation of the contraction order (phi below) baked into the weight packing;
 //  * the weights of one k-step (32 input features x every output tile, in the 3 bf16 planes of
-//    the bf16x6 split) stream through a 3-slot LDS ring by LDS-DMA (two chunks in flight), one
-//    barrier per k-step;
+//    the bf16x6 split) stream through a 2-slot LDS ring by LDS-DMA (one chunk in flight while
+//    one is computed), one barrier per k-step;
 //  * while one wave of a SIMD issues its LDS reads, operand splits, slab stores, DMA pieces or
 //    epilogue, its partner's MFMAs keep the matrix core busy -- the latency hiding that the
 //    one-wave-per-SIMD kernel had to hand-schedule.
@@ -52,9 +52,10 @@ constexpr int kLoaders = LNERF_K16_LOADERS;   // waves that issue the weight DMA
 #ifndef LNERF_K16_NODMA
 #define LNERF_K16_NODMA 0
 #endif
-// chunks in flight while one computes: 1 (waited with vmcnt(0)) measured faster than 2 (a 3-slot
-// ring waited with vmcnt(pending)): 1.96-2.00 vs 2.16 ms
+// chunks in flight while one computes: 1 (a 2-slot ring waited with vmcnt(0)) or 2 (a 3-slot
+// ring waited with a vmcnt that leaves the younger chunk's pieces and the slab stores in flight)
 constexpr int kAhead = LNERF_K16_AHEAD;
+static_assert(kAhead == 1 || kAhead == 2, "the ring has room for two chunks in flight at most");
 constexpr int kSlots = kAhead + 1;            // ring slots
 constexpr int kOffComp = 3 * kSlotBytes;      // room for the deepest ring (kAhead = 2)
 constexpr int kCompBytes = 2688 * 4;          // composite_tile's scratch (comp[0, 2688))
@@ -180,18 +181,17 @@ template <int N>
 __device__ __forceinline__ void vm_wait() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
+// vmcnt(n) for a wave-uniform n (clamped to the 6-bit counter's 63)
+template <int... N>
+__device__ __forceinline__ void vm_wait_n(int n, std::integer_sequence<int, N...>) {
+    n = n > 63 ? 63 : n;
+    ((n == N ? vm_wait<N>() : void()), ...);
+}
 __device__ __forceinline__ void dma_barrier(int pending) {
     PROF_T(t0);
     asm volatile("" ::: "memory");
-    switch (pending) {
-        case 0: vm_wait<0>(); break;
-        case 1: vm_wait<1>(); break;
-        case 2: vm_wait<2>(); break;
-        case 3: vm_wait<3>(); break;
-        case 4: vm_wait<4>(); break;
-        case 5: vm_wait<5>(); break;
-        default: vm_wait<6>(); break;
-    }
+    if (pending == 0) vm_wait<0>();
+    else vm_wait_n(pending, std::make_integer_sequence<int, 64>{});
     PROF_ADD(kPfVm, t0);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -243,18 +243,7 @@ __device__ __forceinline__ void lgkm_wait(bf8 (&w)[3]) {
     asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]) : "n"(N));
 }
 
-template <int N>
-__device__ __forceinline__ void lgkm_wait1(bf8& w) {
-    asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(w) : "n"(N));
-}
-
-#ifndef LNERF_K16_DIST
-#define LNERF_K16_DIST 2
-#endif
-constexpr int kDist = LNERF_K16_DIST;   // weight tiles read ahead of the one the MFMAs consume
-#ifndef LNERF_K16_FINEWAIT
-#define LNERF_K16_FINEWAIT 0           // 1: per-plane lgkmcnt waits inside a tile's MFMAs
-#endif
+constexpr int kDist = 2;   // weight tiles read ahead of the one the MFMAs consume
 
 template <int PL, int O>
 __device__ __forceinline__ void read_tile(unsigned base, bf8 (&w)[3]) {
@@ -273,14 +262,11 @@ __device__ __forceinline__ void tile_step(unsigned base, bf8 (&w)[kDist + 1][3],
     if constexpr (O + kDist < NTO) read_tile<PL, O + kDist>(base, w[(O + kDist) % (kDist + 1)]);
     constexpr int ahead = (NTO - 1 - O) < kDist ? (NTO - 1 - O) : kDist;
     bf8(&c)[3] = w[O % (kDist + 1)];
-    if constexpr (LNERF_K16_FINEWAIT && PL == 3) lgkm_wait1<ahead * PL + 2>(c[0]);
-    else lgkm_wait<ahead * PL>(c);
+    lgkm_wait<ahead * PL>(c);
     fx4 acc = out[O];
     if constexpr (PL == 3) {
         acc = mfma16(c[0], bl, acc);
-        if constexpr (LNERF_K16_FINEWAIT) lgkm_wait1<ahead * PL + 1>(c[1]);
         acc = mfma16(c[1], bm, acc);
-        if constexpr (LNERF_K16_FINEWAIT) lgkm_wait1<ahead * PL>(c[2]);
         acc = mfma16(c[2], bh, acc);
         acc = mfma16(c[1], bh, acc);
         acc = mfma16(c[0], bm, acc);
@@ -299,8 +285,8 @@ __device__ __forceinline__ void tile_steps(std::integer_sequence<int, O...>, uns
 }
 
 // One pass (a layer's forward or backward MMA): out[o] += sum over the pass's k-steps of
-// Wpack[s][o] (x) in[2s..2s+1], NTO output tiles. Chunk ci is read from ring slot ci % 3 while
-// chunks ci+1 (issued one k-step earlier) and ci+2 (issued here) land. `slab` (nullable)
+// Wpack[s][o] (x) in[2s..2s+1], NTO output tiles. Chunk ci is read from ring slot ci % kSlots
+// while chunk ci+kAhead (issued here) lands. `slab` (nullable)
 // receives the input tiles (the A_{l-1} or G_l slab of this wave's half-block).
 template <int NTO, int PL>
 __device__ __forceinline__ void k16_pass(const K16Args& a, int ks, int& ci, unsigned char* ring,
@@ -314,15 +300,16 @@ __device__ __forceinline__ void k16_pass(const K16Args& a, int ks, int& ci, unsi
             // DMA of chunk ci+AHEAD first (its table entry is a scalar load the compiler waits for
             // with lgkmcnt(0), which would also wait for the fragment reads), then the first
             // weight tiles, in flight while the slab stores and the operand split issue
-            const int pending = (LNERF_K16_NODMA && ci >= 2)
-                                    ? 0
-                                    : dma_chunk(a, chunk_at(a, ci + kAhead),
-                                                ring + ((ci + kAhead) % kSlots) * kSlotBytes, bias_ring) *
-                                          (kAhead - 1);
+            // vector-memory operations younger than chunk ci+1's DMA that the barrier may leave in
+            // flight (kAhead = 2): chunk ci+2's pieces and this k-step's 8 slab stores
+            const int issued = (LNERF_K16_NODMA && ci >= 2)
+                                   ? 0
+                                   : dma_chunk(a, chunk_at(a, ci + kAhead),
+                                               ring + ((ci + kAhead) % kSlots) * kSlotBytes, bias_ring);
+            const int pending = kAhead == 1 ? 0 : issued + ((slab && !LNERF_K16_NOSTORE) ? 8 : 0);
             bf8 w[kDist + 1][3];
             read_tile<PL, 0>(base, w[0]);
             if constexpr (NTO > 1) read_tile<PL, 1>(base, w[1]);
-            if constexpr (kDist > 2 && NTO > 2) read_tile<PL, 2>(base, w[2]);
             // (an LDS-transposed form -- 8 ds_write_b32 + 2 ds_read_b128 + 2 dwordx4 stores --
             // measured slower: 2.13-2.18 vs 2.02-2.03 ms)
             if (slab && !LNERF_K16_NOSTORE) store_slab_step(slab + s * 1024, in[2 * s], in[2 * s + 1]);
@@ -340,7 +327,7 @@ __device__ __forceinline__ void k16_pass(const K16Args& a, int ks, int& ci, unsi
                     bh[j] = (__bf16)x;
                 }
             }
-            static_assert(kDist == 2 || kDist == 3, "the prologue reads kDist tiles");
+            static_assert(kDist == 2, "the prologue reads kDist tiles");
             tile_steps<NTO, PL>(std::make_integer_sequence<int, NTO>{}, base, w, bh, bm, bl, out);
             dma_barrier(pending);
             ++ci;

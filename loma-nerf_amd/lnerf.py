@@ -36,8 +36,14 @@ EXPORTED_SYMBOLS = [
     "nerf_evaluate_and_march", "grad_nerf_evaluate_and_march", "mlp_fit", "grad_mlp_fit",
     "mult_a_b", "lnerf_last_error", "lnerf_version", "lnerf_ctx_create", "lnerf_ctx_destroy",
     "lnerf_workspace_bytes", "lnerf_train_step", "lnerf_render", "lnerf_scale_by_device_scalar",
-    "lnerf_adam_update", "lnerf_ctx_timings", "lnerf_get_rays",
+    "lnerf_adam_update", "lnerf_ctx_timings", "lnerf_get_rays", "lnerf_ctx_last_path",
 ]
+
+# lnerf_ctx_last_path bits
+PATH_GENERIC = 1
+PATH_FUSED = 2
+PATH_K16 = 4
+PATH_DW16 = 8
 
 
 class LnerfMLP(ctypes.Structure):
@@ -140,9 +146,10 @@ def configure(lib: ctypes.CDLL) -> None:
                                       ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_float,
                                       ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
     lib.lnerf_ctx_timings.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
+    lib.lnerf_ctx_last_path.argtypes = [ctypes.c_void_p]
     lib.lnerf_get_rays.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(ctypes.c_double), ctypes.c_void_p, ctypes.c_void_p]
-    for name in ("lnerf_ctx_timings", "lnerf_ctx_create", "lnerf_train_step", "lnerf_render",
+    for name in ("lnerf_ctx_timings", "lnerf_ctx_last_path", "lnerf_ctx_create", "lnerf_train_step", "lnerf_render",
                  "lnerf_scale_by_device_scalar", "lnerf_adam_update", "lnerf_get_rays"):
         getattr(lib, name).restype = ctypes.c_int
 
@@ -291,6 +298,14 @@ class Engine:
             raise RuntimeError(f"lnerf_ctx_timings: {last_error()}")
         keys = ("pack", "fused", "loss", "dw", "reduce", "total")
         return {keys[i]: out[i] for i in range(n)}
+
+    def last_path(self) -> dict:
+        """The kernels the last train_step/render ran (lnerf_ctx_last_path)."""
+        v = self.lib.lnerf_ctx_last_path(self.ctx)
+        if v < 0:
+            raise RuntimeError(f"lnerf_ctx_last_path: {last_error()}")
+        return dict(generic=bool(v & PATH_GENERIC), fused=bool(v & PATH_FUSED),
+                    k16=bool(v & PATH_K16), dw16=bool(v & PATH_DW16), planes=(v >> 8) & 3)
 
     def scale_by_device_scalar(self, buf, scale):
         rc = self.lib.lnerf_scale_by_device_scalar(ctypes.c_void_p(buf.data_ptr()), buf.numel(),

@@ -1,0 +1,9 @@
+# round-2 check: GPU tests, then A/B of the product library vs a knob variant
+set -u
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider -x --timeout 120 --timeout-method thread > gpurun_out/t1.log 2>&1
+rc=$?
+echo "pytest rc=$rc"; tail -15 gpurun_out/t1.log
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+bash scripts/gpu_ab.sh "$@"

@@ -103,9 +103,12 @@ def test_fused_nonuniform_widths(engine, prec):
     compare(got, want)
 
 
-def test_fused_deep_mlp(engine):
+@pytest.mark.parametrize("prec", PRECISIONS + [128])
+def test_fused_deep_mlp(engine, prec):
     """12 layers (33->64x11->4): the k16 kernel's chunk stream (2 passes x 11 hidden layers) and
-    its HBM ReLU masks beyond the 8 hidden layers the one-wave kernel keeps in LDS."""
+    its HBM ReLU masks beyond the 8 hidden layers the one-wave kernel keeps in LDS. The bf16
+    precisions must run on k16 (+ dw16 for bf16x6); MFMA_F32 on the one-wave kernel."""
+    import lnerf
     w = nerf_np.make_workload("cfg2", rays=32, samples=32)
     rng = np.random.RandomState(7)
     dims = [33] + [64] * 11 + [4]
@@ -118,9 +121,26 @@ def test_fused_deep_mlp(engine):
         bp[l, :b.shape[0]] = b
     w = nerf_np.Workload(w.pts, w.pts32, w.X, w.dists, w.target, ws, bs, wp, bp, w.F, w.S, w.N)
     w = nerf_np.without_relu_ties(w)
-    got = run_native(engine, w)
+    got = run_native(engine, w, flags=lnerf.FAST | prec)
+    path = engine.last_path()
+    want_planes = {0: 3, 64: 0, 128: 1}[prec]
+    assert path["fused"] and path["planes"] == want_planes, path
+    assert path["k16"] == (prec != 64), path
+    assert path["dw16"] == (prec == 0), path
     want = oracle_ref(w)
-    compare(got, want)
+    if prec == 128:
+        # plain bf16 operands (8 significant bits): a loose sanity bound, not the fp32 tolerance
+        assert abs(got["loss"] - want["loss"]) <= 2e-2 * abs(want["loss"]), (got["loss"], want["loss"])
+        assert_close("dW", got["dW"], want["dW"], rtol=0.0, atol_scale=5e-2)
+    else:
+        compare(got, want)
+
+
+def test_default_path_is_k16_dw16(engine):
+    """The bench configuration (cfg3 MLP) runs k16 + dw16 with the bf16x6 split by default."""
+    w = nerf_np.make_workload("cfg3", rays=8)
+    run_native(engine, w, per_ray=False)
+    assert engine.last_path() == dict(generic=False, fused=True, k16=True, dw16=True, planes=3)
 
 
 def test_fused_ragged_rays_and_samples(engine):

@@ -30,6 +30,7 @@ PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA = f32 vector peak (de
 # x 2.4 GHz = 2516.6 TF; the bf16x6 split spends 6 bf16 MFMA products per fp32 multiply-add
 PEAK_BF16_TFLOPS = 2516.6
 PEAK_X6_TFLOPS = PEAK_BF16_TFLOPS / 6
+PEAK_F16X3_TFLOPS = PEAK_BF16_TFLOPS / 3   # fp16 MFMA runs at the bf16 rate
 PEAK_HBM_GBS = 8000.0
 
 
@@ -50,9 +51,12 @@ def parse():
     ap.add_argument("--render", action="store_true",
                     help="config 5 instead: forward-only eval render of an 800x800 frame at 128 "
                          "samples/ray (bf16 MFMA unless --x6/--mfma-f32), rays sharded over ranks")
-    ap.add_argument("--x6", action="store_true", help="render with the fp32-accurate bf16x6 path")
+    ap.add_argument("--x6", action="store_true",
+                    help="render with the fp32-class default split (fp16x3) instead of plain bf16")
     ap.add_argument("--mfma-f32", action="store_true",
                     help="fused path with exact f32 MFMA products instead of the bf16x6 split")
+    ap.add_argument("--x6-train", action="store_true",
+                    help="fused path with the bf16x6 split instead of the default fp16x3 split")
     return ap.parse_args()
 
 
@@ -155,8 +159,8 @@ def bench_render(args, world, rank, local, dist):
     total = side * side * S
     fwd_flops = 2 * sum(k * n for k, n in shapes)
     if rank == 0:
-        mode = "f32" if args.mfma_f32 else "bf16x6" if args.x6 else "bf16"
-        peak = PEAK_FP32_TFLOPS if args.mfma_f32 else PEAK_X6_TFLOPS if args.x6 else PEAK_BF16_TFLOPS
+        mode = "f32" if args.mfma_f32 else "fp16x3" if args.x6 else "bf16"
+        peak = PEAK_FP32_TFLOPS if args.mfma_f32 else PEAK_F16X3_TFLOPS if args.x6 else PEAK_BF16_TFLOPS
         ach = fwd_flops * N * S / (ms / 1e3) / 1e12
         print(json.dumps({
             "metric": "ray-samples/sec fwd (eval render), 800x800 frame x 128 samples",
@@ -225,6 +229,8 @@ def main():
     flags = lnerf.GENERIC if args.generic else lnerf.FAST
     if args.mfma_f32:
         flags |= lnerf.MFMA_F32
+    elif args.x6_train:
+        flags |= lnerf.MFMA_BF16X6
 
     def step(timing=False):
         f = flags | (lnerf.TIMING if timing else 0)
@@ -278,7 +284,8 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "mfma": ("generic (no MFMA)" if args.generic else "f32" if args.mfma_f32 else
-                     "bf16x6 (fp32 operands split hi+mid+lo, fp32 accumulate)"),
+                     "bf16x6 (fp32 operands split hi+mid+lo, fp32 accumulate)" if args.x6_train else
+                     "fp16x3 (fp32 operands x 2^e split hi+lo in fp16, 3 products, fp32 accumulate)"),
             "data": "synthetic (look-at camera rays, uniform targets, random-init MLP seed 215)",
             "config": {"workload": f"{args.config}: {N} rays x {S} samples per GPU, PE F={b['F']}, "
                                    f"MLP {shapes[0][0]}->{b['H']}x{b['L'] - 1}->4, fp32",
@@ -290,7 +297,8 @@ def main():
         }
         if kt:
             fus_ms = kt["fused"]
-            peak = PEAK_FP32_TFLOPS if args.mfma_f32 else PEAK_X6_TFLOPS
+            peak = (PEAK_FP32_TFLOPS if args.mfma_f32 else PEAK_X6_TFLOPS if args.x6_train
+                    else PEAK_F16X3_TFLOPS)
             # the fused kernel the engine ran: k16 (wave pairs, default for the bf16 planes) or
             # the one-wave-per-SIMD kernel (exact f32 MFMA, or LNERF_K16=0)
             k1 = ("fused_fwd_bwd_kernel" if args.mfma_f32 or os.environ.get("LNERF_K16") == "0"
@@ -303,7 +311,9 @@ def main():
                                "flops_per_launch": fused_flops, "avg_ms": fus_ms,
                                "peak_basis": ("f32 MFMA dense 157.3 TF" if args.mfma_f32 else
                                               "bf16 MFMA dense 2516.6 TF / 6 (bf16x6: six bf16 "
-                                              "products per fp32-accurate multiply-add)")}
+                                              "products per fp32-accurate multiply-add)" if args.x6_train
+                                              else "fp16 MFMA dense 2516.6 TF / 3 (fp16x3: three fp16 "
+                                              "products per multiply-add)")}
             tr = pmc_traffic(k1, args.config) if args.rays is None else None
             if tr:
                 out["roofline"]["traffic"] = tr["bytes"]

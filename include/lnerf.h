@@ -131,10 +131,17 @@ enum {
     LNERF_FAST = 16,          /* require the fused MFMA path (error if the shape is unsupported) */
     LNERF_TIMING = 32,        /* record per-kernel HIP events (read with lnerf_ctx_timings)   */
     LNERF_MFMA_F32 = 64,      /* fused path: exact f32 MFMA products instead of the default
-                                 bf16x6 split (x = hi+mid+lo in bf16, six bf16 MFMAs per
-                                 product, fp32-accurate: dropped terms <= 2^-24 |w x|)         */
-    LNERF_MFMA_BF16 = 128     /* fused path: plain bf16 operands, fp32 accumulate (one MFMA per
+                                 fp16x3 split (below)                                          */
+    LNERF_MFMA_BF16 = 128,    /* fused path: plain bf16 operands, fp32 accumulate (one MFMA per
                                  product; reduced precision -- inference / config 5 render)   */
+    LNERF_MFMA_F16X3 = 256,   /* fused path: the fp16x3 split, the default wherever the k16
+                                 kernel runs: x 2^e = hi + lo in fp16 with per-sample and
+                                 per-layer exponent shifts, three fp16 MFMAs per product
+                                 (dropped terms <= ~3 2^-22 |w x|, the precision of 3xTF32),
+                                 fp32 accumulate                                               */
+    LNERF_MFMA_BF16X6 = 512   /* fused path: the bf16x6 split (x = hi+mid+lo in bf16, six bf16
+                                 MFMAs per product, dropped terms <= 2^-24 |w x|); the default
+                                 where k16 does not run (LNERF_K16=0, heads over 16 outputs) */
 };
 
 /* Optional outputs (device pointers; any may be NULL). */

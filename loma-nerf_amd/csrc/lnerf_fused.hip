@@ -1613,7 +1613,7 @@ size_t fused_workspace_bytes(const lnerf_mlp& m, int rays, int S, bool train) {
                align_up(y.act_total, 64) + align_up(y.grad_total, 64) +
                align_up((size_t)y.num_wg, 64) + align_up(y.dwp_total, 64) + align_up(y.dbp_total, 64) +
                64 + align_up((y.w16_total + 1) / 2, 64) + align_up(y.b16_total, 64) +
-               align_up(y.mask_total * 2, 64);
+               align_up(y.mask_total * 2, 64) + 64;   // + the fp16x3 weight exponent shifts
     return f * sizeof(float);
 }
 
@@ -1623,14 +1623,17 @@ void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws
     make_layout(y, m, b.rays, b.samples, train);
     p.L = m.num_layers;
     p.ht = y.ht;
-    // The bf16 planes run on k16 (ReLU masks in HBM, any depth) unless LNERF_K16=0 or the head
+    // The bf16/fp16 planes run on k16 (ReLU masks in HBM, any depth) unless LNERF_K16=0 or the head
     // is wider than one 16-wide tile; only the one-wave kernel keeps its masks in LDS, 1 KiB per
     // hidden layer and wave in the bf16x6 budget: (L-1) <= kMaskTiles / 8. Past that depth the
     // one-wave kernel falls back to exact f32 products.
     const char* e = getenv("LNERF_K16");
     const bool k16_wanted = !(e && e[0] == '0') && !(flags & LNERF_MFMA_F32) && m.n[p.L - 1] <= 16;
     const bool bf_ok = k16_wanted || (p.L - 1) <= kMaskTiles(true) / 8;
-    p.x6 = (flags & LNERF_MFMA_F32) || !bf_ok ? 0 : (flags & LNERF_MFMA_BF16) ? 1 : 3;
+    p.x6 = (flags & LNERF_MFMA_F32) || !bf_ok ? 0
+           : (flags & LNERF_MFMA_BF16)        ? 1
+           : (flags & LNERF_MFMA_BF16X6) || !k16_wanted ? 3
+                                                        : 2;   // fp16x3 (k16 only)
     for (int l = 0; l < p.L; ++l) {
         p.fo[l] = y.fo[l];
         p.bo[l] = y.bo[l];
@@ -1693,6 +1696,8 @@ void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws
     off += align_up(y.b16_total, 64);
     p.mask_g = (unsigned long long*)(base + off);
     off += align_up(y.mask_total * 2, 64);
+    p.wexp16 = (int*)(base + off);
+    off += 64;
 
     p.x_off = y.x_off;
     p.ht16 = y.ht16;
@@ -1709,7 +1714,7 @@ void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws
     p.k16 = k16_wanted && k16_supported(p) ? 1 : 0;
     // dW: dw16_kernel for the bf16x6 split (LNERF_DW16=0: dw_all_kernel); one partial per split
     const char* e2 = getenv("LNERF_DW16");
-    p.dw16 = (e2 && e2[0] == '0') ? 0 : (p.x6 == 3 ? 1 : 0);
+    p.dw16 = (e2 && e2[0] == '0') ? 0 : (p.x6 == 3 || p.x6 == 2 ? 1 : 0);
     if (p.dw16)
         for (int l = 0; l < p.L; ++l) p.dw_phases[l] = 1;
 }

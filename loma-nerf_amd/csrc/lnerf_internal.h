@@ -127,8 +127,9 @@ struct FusedPlan {
     float* bp;        // biases in fragment order
     size_t wf_off[kMaxLayers], wb_off[kMaxLayers], bp_off[kMaxLayers];
     int ht;           // hidden output tiles (1/2/4/8): the fused kernel's instantiation
-    int x6;           // bf16 planes per operand: 3 = bf16x6 split (fp32-accurate), 1 = bf16,
-                      // 0 = exact f32 MFMA
+    int x6;           // planes per operand: 3 = bf16x6 split (fp32-accurate), 2 = fp16x3 split
+                      // (fp16 hi + lo with exponent shifts, 22-bit products; k16 only),
+                      // 1 = bf16, 0 = exact f32 MFMA
     int fo[kMaxLayers], bo[kMaxLayers];  // packed output tiles of each layer's fwd / bwd MMA
     unsigned short* w6;                  // bf16x6 packed planes (u16 offsets below)
     size_t w6f_off[kMaxLayers], w6b_off[kMaxLayers], w6f_n[kMaxLayers], w6b_n[kMaxLayers];
@@ -158,6 +159,7 @@ struct FusedPlan {
     float* b16;                          // [L][256] zero-padded biases
     unsigned long long* mask_g;          // [num_wg][L-1][8 waves][64 lanes] ReLU mask bits
     int dw16;                            // 1: dW by dw16_kernel (lnerf_dw16.hip), one partial per split
+    int* wexp16;                         // x6 = 2: per-layer exponent shift of the fp16 weight planes
 };
 
 bool fused_supported(const lnerf_mlp& mlp, int rays, int S, int input_mode, const char** why);

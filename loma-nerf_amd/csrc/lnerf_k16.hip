@@ -31,6 +31,7 @@ namespace {
 
 typedef float fx4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef _Float16 hf8 __attribute__((ext_vector_type(8)));
 
 constexpr int kThreads = 512;
 constexpr int kWaves = 8;
@@ -38,13 +39,27 @@ constexpr int kTile = comp::kTileSamples;     // 128 samples per workgroup
 constexpr int kMaxChunks = 2 * kMaxLayers * 8 + 2;   // <= 2 passes x 8 k-steps per layer + 2 end
 constexpr int kMaxT = 16;                     // 16-feature tiles per 256-wide layer
 constexpr int kSlotBytes = kMaxT * 3 * 1024;  // one k-step of a 256-output layer, 3 planes
+// ring slot of a PL-plane kernel: one k-step of a 256-output layer
+template <int PL>
+constexpr int slot_bytes() { return kMaxT * PL * 1024; }
+// Staggered wave pairs (default): waves 0-3 ("early") meet the per-chunk barrier at the end of
+// a chunk, waves 4-7 ("late", each the SIMD partner of an early wave) in its middle, so the two
+// waves of a SIMD run their chunk prologues (DMA issue, slab stores, operand split, first
+// fragment reads) half a chunk apart, each under its partner's MFMAs. The ring then needs 3
+// slots: in one barrier period the late waves still read the previous chunk's second half while
+// every wave reads the current chunk and the next one lands (one chunk in flight; every wave
+// issues 1/8 of its pieces right after its own prologue).
+#ifndef LNERF_K16_STAGGER
+#define LNERF_K16_STAGGER 1
+#endif
+constexpr bool kStagger = LNERF_K16_STAGGER != 0;
 #ifndef LNERF_K16_AHEAD
 #define LNERF_K16_AHEAD 1
 #endif
 #ifndef LNERF_K16_LOADERS
 #define LNERF_K16_LOADERS 4
 #endif
-constexpr int kLoaders = LNERF_K16_LOADERS;   // waves that issue the weight DMA
+constexpr int kLoaders = kStagger ? 8 : LNERF_K16_LOADERS;   // waves that issue the weight DMA
 // timing experiments only (wrong results): drop the slab stores / the weight DMA after chunk 2
 #ifndef LNERF_K16_NOSTORE
 #define LNERF_K16_NOSTORE 0
@@ -52,12 +67,12 @@ constexpr int kLoaders = LNERF_K16_LOADERS;   // waves that issue the weight DMA
 #ifndef LNERF_K16_NODMA
 #define LNERF_K16_NODMA 0
 #endif
-// chunks in flight while one computes: 1 (a 2-slot ring waited with vmcnt(0)) or 2 (a 3-slot
-// ring waited with a vmcnt that leaves the younger chunk's pieces and the slab stores in flight)
-constexpr int kAhead = LNERF_K16_AHEAD;
+// unstaggered: chunks in flight while one computes: 1 (a 2-slot ring) or 2 (a 3-slot ring;
+// measured slower)
+constexpr int kAhead = kStagger ? 1 : LNERF_K16_AHEAD;
 static_assert(kAhead == 1 || kAhead == 2, "the ring has room for two chunks in flight at most");
-constexpr int kSlots = kAhead + 1;            // ring slots
-constexpr int kOffComp = 3 * kSlotBytes;      // room for the deepest ring (kAhead = 2)
+constexpr int kSlots = kStagger ? 3 : kAhead + 1;   // ring slots
+constexpr int kOffComp = 3 * kSlotBytes;      // room for the deepest ring
 constexpr int kCompBytes = 2688 * 4;          // composite_tile's scratch (comp[0, 2688))
 constexpr int kOffRay = kOffComp + kCompBytes;
 constexpr int kOffBias = kOffRay + kTile * 4;
@@ -95,6 +110,7 @@ struct K16Args {
     float seed;
     int want_grad;
     int planes;
+    const int* wexp;   // PL = 2: per-layer max|W| bits of the packed fp16 weight planes (wshift_of)
 };
 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
@@ -187,11 +203,13 @@ __device__ __forceinline__ void vm_wait_n(int n, std::integer_sequence<int, N...
     n = n > 63 ? 63 : n;
     ((n == N ? vm_wait<N>() : void()), ...);
 }
+// pending < 0: this wave has no DMA piece to wait for (only the barrier)
 __device__ __forceinline__ void dma_barrier(int pending) {
     PROF_T(t0);
     asm volatile("" ::: "memory");
     if (pending == 0) vm_wait<0>();
-    else vm_wait_n(pending, std::make_integer_sequence<int, 64>{});
+    else if (pending == 8) vm_wait<8>();   // kAhead = 1: a loader wave behind its slab stores
+    else if (pending > 0) vm_wait_n(pending, std::make_integer_sequence<int, 64>{});
     PROF_ADD(kPfVm, t0);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -200,6 +218,29 @@ __device__ __forceinline__ void dma_barrier(int pending) {
 
 __device__ __forceinline__ fx4 mfma16(const bf8& a, const bf8& b, fx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// the same fragments as fp16 (PL = 2: the fp16x3 planes)
+__device__ __forceinline__ fx4 mfma16h(const bf8& a, const bf8& b, fx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(hf8, a), __builtin_bit_cast(hf8, b), c, 0, 0,
+                                                  0);
+}
+
+// fp16x3 (PL = 2): x * 2^e = hi + lo, round-to-nearest fp16 of each (the remainder is exact in
+// f32); |x 2^e - hi - lo| <= 2^-22 |x 2^e|. The exponent shift keeps the operand's largest value
+// in [2^13, 2^14), inside fp16's range (the 3xTF32 split of CUTLASS, on fp16 pieces).
+__device__ __forceinline__ void split_h(float xs, _Float16& h, _Float16& l) {
+    h = (_Float16)xs;
+    l = (_Float16)(xs - (float)h);
+}
+
+// the exponent shift ew of a layer from its max|W| bits: max|W| 2^ew in [2^13, 2^14) (0 for an
+// all-zero or non-finite layer) -- the weight-side half of the fp16x3 scaling
+__device__ __forceinline__ int wshift_of(int maxbits) {
+    const float mx = __int_as_float(maxbits);
+    if (!(mx > 0.0f) || !(mx < __builtin_inff())) return 0;
+    int e;
+    (void)__builtin_frexpf(mx, &e);
+    return 14 - e;
 }
 
 // x = hi + mid + lo (round-to-nearest bf16 of each remainder; every remainder is exact in f32)
@@ -248,10 +289,8 @@ constexpr int kDist = 2;   // weight tiles read ahead of the one the MFMAs consu
 template <int PL, int O>
 __device__ __forceinline__ void read_tile(unsigned base, bf8 (&w)[3]) {
     w[0] = ds_read_at<(O * PL + 0) * 1024>(base);
-    if constexpr (PL == 3) {
-        w[1] = ds_read_at<(O * PL + 1) * 1024>(base);
-        w[2] = ds_read_at<(O * PL + 2) * 1024>(base);
-    }
+    if constexpr (PL >= 2) w[1] = ds_read_at<(O * PL + 1) * 1024>(base);
+    if constexpr (PL == 3) w[2] = ds_read_at<(O * PL + 2) * 1024>(base);
 }
 
 // Output tile O of one k-step: issue the reads of tile O + kDist, wait for tile O's (leaving
@@ -264,7 +303,12 @@ __device__ __forceinline__ void tile_step(unsigned base, bf8 (&w)[kDist + 1][3],
     bf8(&c)[3] = w[O % (kDist + 1)];
     lgkm_wait<ahead * PL>(c);
     fx4 acc = out[O];
-    if constexpr (PL == 3) {
+    if constexpr (PL == 2) {
+        // fp16x3: small terms first (w_hi x_lo, w_lo x_hi), then w_hi x_hi; (bh, bm) = (x_hi, x_lo)
+        acc = mfma16h(c[0], bm, acc);
+        acc = mfma16h(c[1], bh, acc);
+        acc = mfma16h(c[0], bh, acc);
+    } else if constexpr (PL == 3) {
         acc = mfma16(c[0], bl, acc);
         acc = mfma16(c[1], bm, acc);
         acc = mfma16(c[2], bh, acc);
@@ -277,11 +321,12 @@ __device__ __forceinline__ void tile_step(unsigned base, bf8 (&w)[kDist + 1][3],
     out[O] = acc;
 }
 
-template <int NTO, int PL, int... O>
+// tiles B, B+1, ... of one k-step
+template <int NTO, int PL, int B, int... O>
 __device__ __forceinline__ void tile_steps(std::integer_sequence<int, O...>, unsigned base,
                                            bf8 (&w)[kDist + 1][3], const bf8& bh, const bf8& bm,
                                            const bf8& bl, fx4 (&out)[kMaxT]) {
-    (tile_step<NTO, PL, O>(base, w, bh, bm, bl, out), ...);
+    (tile_step<NTO, PL, B + O>(base, w, bh, bm, bl, out), ...);
 }
 
 // One pass (a layer's forward or backward MMA): out[o] += sum over the pass's k-steps of
@@ -291,22 +336,30 @@ __device__ __forceinline__ void tile_steps(std::integer_sequence<int, O...>, uns
 template <int NTO, int PL>
 __device__ __forceinline__ void k16_pass(const K16Args& a, int ks, int& ci, unsigned char* ring,
                                          float* bias_ring, const fx4 (&in)[kMaxT], fx4 (&out)[kMaxT],
-                                         float* __restrict__ slab) {
+                                         float* __restrict__ slab, int ex = 0) {
     const int lane = threadIdx.x & 63;
+    constexpr int kSB = slot_bytes<PL>();
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
         if (s < ks) {
-            const unsigned base = lds_addr(ring + (ci % kSlots) * kSlotBytes) + lane * 16;
+            const unsigned base = lds_addr(ring + (ci % kSlots) * kSB) + lane * 16;
             // DMA of chunk ci+AHEAD first (its table entry is a scalar load the compiler waits for
             // with lgkmcnt(0), which would also wait for the fragment reads), then the first
             // weight tiles, in flight while the slab stores and the operand split issue
-            // vector-memory operations younger than chunk ci+1's DMA that the barrier may leave in
-            // flight (kAhead = 2): chunk ci+2's pieces and this k-step's 8 slab stores
+            // The barrier waits for this wave's pieces of chunk ci+1 only: the vector-memory
+            // operations younger than them stay in flight -- this k-step's 8 slab stores and
+            // (kAhead = 2) chunk ci+2's pieces. A wave that issues no DMA does not wait at all
+            // (its slab stores need no completion before the barrier).
             const int issued = (LNERF_K16_NODMA && ci >= 2)
                                    ? 0
                                    : dma_chunk(a, chunk_at(a, ci + kAhead),
-                                               ring + ((ci + kAhead) % kSlots) * kSlotBytes, bias_ring);
-            const int pending = kAhead == 1 ? 0 : issued + ((slab && !LNERF_K16_NOSTORE) ? 8 : 0);
+                                               ring + ((ci + kAhead) % kSlots) * kSB, bias_ring);
+            asm volatile("" ::: "memory");   // the slab stores stay younger than the pieces
+            const int nst = (slab && !LNERF_K16_NOSTORE) ? 8 : 0;
+            const int pending = wave_id() >= kLoaders ? -1
+                                : kAhead == 1       ? (issued ? nst : -1)
+                                                    : issued + nst;
+            const bool late = kStagger && wave_id() >= 4;
             bf8 w[kDist + 1][3];
             read_tile<PL, 0>(base, w[0]);
             if constexpr (NTO > 1) read_tile<PL, 1>(base, w[1]);
@@ -323,13 +376,22 @@ __device__ __forceinline__ void k16_pass(const K16Args& a, int ks, int& ci, unsi
                     bh[j] = h;
                     bm[j] = m;
                     bl[j] = l;
+                } else if (PL == 2) {
+                    _Float16 h, l;
+                    split_h(__builtin_ldexpf(x, ex), h, l);
+                    bh[j] = __builtin_bit_cast(__bf16, h);
+                    bm[j] = __builtin_bit_cast(__bf16, l);
                 } else {
                     bh[j] = (__bf16)x;
                 }
             }
             static_assert(kDist == 2, "the prologue reads kDist tiles");
-            tile_steps<NTO, PL>(std::make_integer_sequence<int, NTO>{}, base, w, bh, bm, bl, out);
-            dma_barrier(pending);
+            // first half of the output tiles, [late waves: barrier], second half, [early: barrier]
+            constexpr int H = (NTO + 1) / 2;
+            tile_steps<NTO, PL, 0>(std::make_integer_sequence<int, H>{}, base, w, bh, bm, bl, out);
+            if (late) dma_barrier(pending);
+            tile_steps<NTO, PL, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, bh, bm, bl, out);
+            if (!late) dma_barrier(pending);
             ++ci;
         }
     }
@@ -338,12 +400,30 @@ __device__ __forceinline__ void k16_pass(const K16Args& a, int ks, int& ci, unsi
 template <int PL>
 __device__ __forceinline__ void k16_pass_n(const K16Args& a, int ks, int& ci, unsigned char* ring,
                                            float* bias_ring, int nto, const fx4 (&in)[kMaxT],
-                                           fx4 (&out)[kMaxT], float* slab) {
-    if (nto <= 1) k16_pass<1, PL>(a, ks, ci, ring, bias_ring, in, out, slab);
-    else if (nto <= 2) k16_pass<2, PL>(a, ks, ci, ring, bias_ring, in, out, slab);
-    else if (nto <= 4) k16_pass<4, PL>(a, ks, ci, ring, bias_ring, in, out, slab);
-    else if (nto <= 8) k16_pass<8, PL>(a, ks, ci, ring, bias_ring, in, out, slab);
-    else k16_pass<16, PL>(a, ks, ci, ring, bias_ring, in, out, slab);
+                                           fx4 (&out)[kMaxT], float* slab, int ex) {
+    if (nto <= 1) k16_pass<1, PL>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
+    else if (nto <= 2) k16_pass<2, PL>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
+    else if (nto <= 4) k16_pass<4, PL>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
+    else if (nto <= 8) k16_pass<8, PL>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
+    else k16_pass<16, PL>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
+}
+
+// PL = 2: the per-sample exponent shift of a pass's input (lanes n, n + 16, n + 32, n + 48 hold
+// sample n's features): max|x| 2^ex in [2^13, 2^14); 0 for an all-zero (or non-finite) sample.
+template <int PL>
+__device__ __forceinline__ int sample_shift(const fx4 (&in)[kMaxT]) {
+    if constexpr (PL != 2) return 0;
+    float m = 0.0f;
+#pragma unroll
+    for (int o = 0; o < kMaxT; ++o)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) m = __builtin_fmaxf(m, __builtin_fabsf(in[o][i]));
+    m = __builtin_fmaxf(m, __shfl_xor(m, 16));
+    m = __builtin_fmaxf(m, __shfl_xor(m, 32));
+    if (!(m > 0.0f) || !(m < __builtin_inff())) return 0;
+    int e;
+    (void)__builtin_frexpf(m, &e);   // m = f 2^e, f in [0.5, 1)
+    return 14 - e;
 }
 
 // The layer's biases in the accumulator layout (fx4 = 4 consecutive features of a lane group),
@@ -373,8 +453,8 @@ __device__ __forceinline__ void zero_tiles(fx4 (&t)[kMaxT]) {
     for (int o = 0; o < kMaxT; ++o) t[o] = fx4{0.0f, 0.0f, 0.0f, 0.0f};
 }
 
-// HT: 16-wide output tiles of every hidden layer (1/2/4/8/16); PL: bf16 planes (3 = bf16x6,
-// fp32-accurate; 1 = plain bf16, inference).
+// HT: 16-wide output tiles of every hidden layer (1/2/4/8/16); PL: operand planes (3 = bf16x6,
+// 2 = fp16x3, both fp32-class; 1 = plain bf16, inference).
 template <int HT, int PL>
 __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
     __shared__ __attribute__((aligned(16))) unsigned char lds[kLdsBytes];
@@ -400,6 +480,12 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
 
     fx4 act[kMaxT], out[kMaxT];
     zero_tiles(act);
+    // PL = 2: layer l's weight exponent shift in lane l (read with readlane per pass); a pass's
+    // accumulators carry 2^(ex + ew), removed exactly (powers of two) in its epilogue
+    const int wexp_lane = (PL == 2 && lane < a.L) ? wshift_of(a.wexp[lane]) : 0;
+    auto unscale = [&](int l, int ex) -> int {
+        return PL == 2 ? -(ex + __builtin_amdgcn_readlane(wexp_lane, l)) : 0;
+    };
 
     // ---- layer-0 input in the accumulator layout, through a per-wave LDS scratch (the ring is
     // free before the first DMA). POINTS/RAYS with k0 <= 64: one float64 sincos per (sample,
@@ -449,7 +535,7 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
 
     int ci = 0;   // chunk stream position (chunk_at)
     dma_chunk(a, chunk_at(a, 0), ring, bias_ring);
-    dma_barrier(kAhead == 2 ? dma_chunk(a, chunk_at(a, 1), ring + kSlotBytes, bias_ring) : 0);
+    dma_barrier(kAhead == 2 ? dma_chunk(a, chunk_at(a, 1), ring + slot_bytes<PL>(), bias_ring) : 0);
     PROF_ADD(kPfPE, t_start);
     // ReLU mask bits of this wave, per hidden layer: [L-1][lane] u64
     unsigned long long* mask_w = a.mask_g + ((size_t)wg * (a.L - 1) * kWaves + wave) * 64 + lane;
@@ -462,9 +548,11 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
                                 half * 512;
         zero_tiles(out);
         const unsigned bl = lds_addr(bias_ring + (l % 3) * 256) + g * 16;
+        const int ex = sample_shift<PL>(act);
+        const int sh = unscale(l, ex);
         if (l < a.L - 1) {
             PROF_T(t_f);
-            k16_pass<HT, PL>(a, a.ks_f[l], ci, ring, bias_ring, act, out, slab);
+            k16_pass<HT, PL>(a, a.ks_f[l], ci, ring, bias_ring, act, out, slab, ex);
             PROF_ADD(kPfFwd, t_f);
             PROF_T(t_fe);
             // bias after the sum (nerf.py:98,125), ReLU (nerf.py:141-144) and its mask bits
@@ -476,7 +564,7 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
             for (int o = 0; o < HT; ++o) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const float v = out[o][i] + bv[o][i];
+                    const float v = (PL == 2 ? __builtin_ldexpf(out[o][i], sh) : out[o][i]) + bv[o][i];
                     const bool pos = v > 0.0f;
                     act[o][i] = pos ? v : 0.0f;
                     mb |= (pos ? 1ull : 0ull) << (4 * o + i);
@@ -485,14 +573,15 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
             if (st) mask_w[(size_t)l * kWaves * 64] = mb;
             PROF_ADD(kPfFwdEpi, t_fe);
         } else {
-            k16_pass<1, PL>(a, a.ks_f[l], ci, ring, bias_ring, act, out, slab);
+            k16_pass<1, PL>(a, a.ks_f[l], ci, ring, bias_ring, act, out, slab, ex);
             fx4 bv[kMaxT];
             bias_read<1>(std::make_integer_sequence<int, 1>{}, bl, bv);
             bias_wait<1>(std::make_integer_sequence<int, 1>{}, bv);
             // head pre-activations: features 0..3 = registers 0..3 of lane group 0
             if (g == 0) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) comp[ls * 4 + i] = out[0][i] + bv[0][i];
+                for (int i = 0; i < 4; ++i)
+                    comp[ls * 4 + i] = (PL == 2 ? __builtin_ldexpf(out[0][i], sh) : out[0][i]) + bv[0][i];
             }
         }
     }
@@ -522,13 +611,17 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
         float* slab = a.grad + a.grad_off[l] + blk * (size_t)(a.nt[l] * 1024) + half * 512;
         PROF_T(t_b);
         const unsigned long long mb = mask_w[(size_t)(l - 1) * kWaves * 64];   // in flight over the pass
-        k16_pass<HT, PL>(a, a.ks_b[l], ci, ring, bias_ring, act, out, slab);
+        const int ex = sample_shift<PL>(act);
+        const int sh = unscale(l, ex);
+        k16_pass<HT, PL>(a, a.ks_b[l], ci, ring, bias_ring, act, out, slab, ex);
         PROF_ADD(kPfBwd, t_b);
         PROF_T(t_be);
 #pragma unroll
         for (int o = 0; o < HT; ++o)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) act[o][i] = ((mb >> (4 * o + i)) & 1ull) ? out[o][i] : 0.0f;
+            for (int i = 0; i < 4; ++i)
+                act[o][i] = ((mb >> (4 * o + i)) & 1ull) ? (PL == 2 ? __builtin_ldexpf(out[o][i], sh) : out[o][i])
+                                                         : 0.0f;
         PROF_ADD(kPfBwdEpi, t_be);
     }
     PROF_T(t_t);
@@ -537,7 +630,9 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
     if (a.d_x) {
         // d_layer_input = G_0 W_0^T (ENCODED mode); the pass also writes G_0's slab
         zero_tiles(out);
-        k16_pass_n<PL>(a, a.ks_b[0], ci, ring, bias_ring, a.to_b[0], act, out, g0);
+        const int ex = sample_shift<PL>(act);
+        const int sh = unscale(0, ex);
+        k16_pass_n<PL>(a, a.ks_b[0], ci, ring, bias_ring, a.to_b[0], act, out, g0, ex);
         if (valid) {
 #pragma unroll
             for (int o = 0; o < kMaxT; ++o)
@@ -545,7 +640,7 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         const int f = 16 * o + 4 * g + i;
-                        if (f < a.k0) a.d_x[(size_t)gs * a.k0 + f] = out[o][i];
+                        if (f < a.k0) a.d_x[(size_t)gs * a.k0 + f] = PL == 2 ? __builtin_ldexpf(out[o][i], sh) : out[o][i];
                     }
                 }
         }
@@ -575,7 +670,28 @@ struct Pack16Args {
     unsigned short* w16;
     size_t wf_off[kMaxLayers], wb_off[kMaxLayers];
     float* b16;
+    int* wexp;   // planes = 2: per-layer max|W| bits (wmax16_kernel)
 };
+
+// planes = 2: max|W_l| per layer as the bits of a non-negative float (integer order = float
+// order), grid (64, L): each block folds its rows into one atomicMax on a.wexp[l] (zeroed first).
+__global__ void wmax16_kernel(Pack16Args a) {
+    const int l = blockIdx.y;
+    const float* W = a.W + (size_t)l * a.w_k * a.w_n;
+    const int K = a.k[l], N = a.n[l];
+    float m = 0.0f;
+    for (int k = blockIdx.x; k < K; k += gridDim.x)
+        for (int j = threadIdx.x; j < N; j += blockDim.x) m = fmaxf(m, fabsf(W[(size_t)k * a.w_n + j]));
+    __shared__ float red[256];
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + w]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && red[0] > 0.0f) atomicMax(&a.wexp[l], __float_as_int(red[0]));
+}
+
 
 __global__ void pack16_kernel(Pack16Args a, int l) {
     const float* W = a.W + (size_t)l * a.w_k * a.w_n;
@@ -598,10 +714,17 @@ __global__ void pack16_kernel(Pack16Args a, int l) {
         const int f = phi(s, ln >> 4, j), m = 16 * o + (ln & 15);
         const int kk = fwd ? f : m, jj = fwd ? m : f;
         const float w = (kk < K && jj < N) ? W[(size_t)kk * a.w_n + jj] : 0.0f;
-        __bf16 h, mi, lo;
-        split_x(w, h, mi, lo);
         unsigned short* dst = a.w16 + (fwd ? a.wf_off[l] : a.wb_off[l]) +
                               ((size_t)(s * to + o) * a.planes) * 512 + ln * 8 + j;
+        if (a.planes == 2) {
+            _Float16 h, lo;
+            split_h(__builtin_ldexpf(w, wshift_of(a.wexp[l])), h, lo);
+            dst[0] = __builtin_bit_cast(unsigned short, h);
+            dst[512] = __builtin_bit_cast(unsigned short, lo);
+            continue;
+        }
+        __bf16 h, mi, lo;
+        split_x(w, h, mi, lo);
         dst[0] = __builtin_bit_cast(unsigned short, h);
         if (a.planes == 3) {
             dst[512] = __builtin_bit_cast(unsigned short, mi);
@@ -613,7 +736,7 @@ __global__ void pack16_kernel(Pack16Args a, int l) {
 }  // namespace
 
 bool k16_supported(const FusedPlan& p) {
-    if (p.x6 != 3 && p.x6 != 1) return false;
+    if (p.x6 != 3 && p.x6 != 2 && p.x6 != 1) return false;
     if (p.n[p.L - 1] > 16) return false;       // head: one 16-wide output tile
     return true;
 }
@@ -638,6 +761,11 @@ void k16_pack(const FusedPlan& p, const float* ws, const float* bs, hipStream_t 
     a.B = bs;
     a.w16 = p.w16;
     a.b16 = p.b16;
+    a.wexp = p.wexp16;
+    if (a.planes == 2) {
+        (void)hipMemsetAsync(p.wexp16, 0, sizeof(int) * p.L, s);
+        wmax16_kernel<<<dim3(64, p.L), 256, 0, s>>>(a);
+    }
     for (int l = 0; l < p.L; ++l) {
         const size_t nel = ((size_t)a.ks_f[l] * a.to_f[l] + (size_t)a.ks_b[l] * a.to_b[l]) * 512 + 256;
         pack16_kernel<<<(unsigned)((nel + 255) / 256), 256, 0, s>>>(a, l);
@@ -686,6 +814,7 @@ void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lner
     a.seed = seed;
     a.want_grad = want_grad ? 1 : 0;
     a.planes = p.x6;
+    a.wexp = p.wexp16;
     // the chunk stream: forward 0..L-1, backward L-1..1 (training), backward 0 (d_x)
     {
         int ci = 0;
@@ -705,6 +834,7 @@ void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lner
     static_assert(sizeof(K16Args) <= 4096, "kernel arguments");
 #define LNERF_K16_LAUNCH(HT)                                                              \
     if (p.x6 == 3) k16_fwd_bwd_kernel<HT, 3><<<p.num_wg, kThreads, 0, s>>>(a);            \
+    else if (p.x6 == 2) k16_fwd_bwd_kernel<HT, 2><<<p.num_wg, kThreads, 0, s>>>(a);       \
     else k16_fwd_bwd_kernel<HT, 1><<<p.num_wg, kThreads, 0, s>>>(a);
     switch (p.ht16) {
         case 1: LNERF_K16_LAUNCH(1) break;

@@ -28,8 +28,10 @@ WANT_DX = 4
 GENERIC = 8
 FAST = 16
 TIMING = 32
-MFMA_F32 = 64     # fused path: exact f32 MFMA instead of the bf16x6 split
+MFMA_F32 = 64     # fused path: exact f32 MFMA instead of the default fp16x3 split
 MFMA_BF16 = 128   # fused path: plain bf16 operands (reduced precision; inference)
+MFMA_F16X3 = 256  # fused path: fp16x3 split (22-bit products, fp32 accumulate; the k16 default)
+MFMA_BF16X6 = 512  # fused path: bf16x6 split (fp32-accurate products)
 
 # every symbol include/lnerf.h declares (tests check the library exports all of them)
 EXPORTED_SYMBOLS = [

@@ -4,8 +4,10 @@ size-independent properties at the full bench size (4096 rays x 64 samples, 8x25
 Tolerance (fp32, north_star "within 1e-4"): |got - want| <= 1e-4 |want| + 1e-4 max|want| per
 tensor. The fused path sums in a different order than the scalar loma-order oracle (MFMA k-order,
 split-K over samples), so it is not bit-exact; sample/ray indexing is exact by construction
-(tested with per-ray outputs). Both fused precisions are checked: the default bf16x6 split
-(fp32-accurate products on the bf16 MFMA) and the exact f32 MFMA (LNERF_MFMA_F32).
+(tested with per-ray outputs). Every fused precision is checked: the default fp16x3 split
+(22-bit products on the fp16 MFMA with per-sample / per-layer exponent shifts), the bf16x6 split
+(fp32-accurate products on the bf16 MFMA, LNERF_MFMA_BF16X6) and the exact f32 MFMA
+(LNERF_MFMA_F32).
 """
 import numpy as np
 import pytest
@@ -60,7 +62,7 @@ def compare(got, want, keys=("dW", "dB", "d_dists", "d_target"), tol=TOL):
         assert_close(k, got[k], want[k], **tol)
 
 
-PRECISIONS = [0, 64]   # default bf16x6 split, lnerf.MFMA_F32
+PRECISIONS = [0, 64, 512]   # default (fp16x3 split), lnerf.MFMA_F32, lnerf.MFMA_BF16X6
 
 
 @pytest.mark.parametrize("prec", PRECISIONS)
@@ -123,10 +125,10 @@ def test_fused_deep_mlp(engine, prec):
     w = nerf_np.without_relu_ties(w)
     got = run_native(engine, w, flags=lnerf.FAST | prec)
     path = engine.last_path()
-    want_planes = {0: 3, 64: 0, 128: 1}[prec]
+    want_planes = {0: 2, 64: 0, 128: 1, 512: 3}[prec]
     assert path["fused"] and path["planes"] == want_planes, path
     assert path["k16"] == (prec != 64), path
-    assert path["dw16"] == (prec == 0), path
+    assert path["dw16"] == (prec in (0, 512)), path
     want = oracle_ref(w)
     if prec == 128:
         # plain bf16 operands (8 significant bits): a loose sanity bound, not the fp32 tolerance
@@ -137,10 +139,18 @@ def test_fused_deep_mlp(engine, prec):
 
 
 def test_default_path_is_k16_dw16(engine):
-    """The bench configuration (cfg3 MLP) runs k16 + dw16 with the bf16x6 split by default."""
+    """The bench configuration (cfg3 MLP) runs k16 + dw16 with the fp16x3 split by default, and
+    the one-wave kernel with the bf16x6 split when k16 is switched off."""
+    import os
     w = nerf_np.make_workload("cfg3", rays=8)
     run_native(engine, w, per_ray=False)
-    assert engine.last_path() == dict(generic=False, fused=True, k16=True, dw16=True, planes=3)
+    assert engine.last_path() == dict(generic=False, fused=True, k16=True, dw16=True, planes=2)
+    os.environ["LNERF_K16"] = "0"
+    try:
+        run_native(engine, w, per_ray=False)
+        assert engine.last_path() == dict(generic=False, fused=True, k16=False, dw16=True, planes=3)
+    finally:
+        del os.environ["LNERF_K16"]
 
 
 def test_fused_ragged_rays_and_samples(engine):

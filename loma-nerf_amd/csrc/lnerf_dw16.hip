@@ -1,6 +1,6 @@
 // lnerf_dw16.hip -- k2 on wave pairs: dW_l = sum_s A_{l-1}[s]^T G_l[s] and db_l = sum_s G_l[s]
-// from the slabs k1 wrote, bf16x6 (fp32-accurate) on v_mfma_f32_32x32x16_bf16, two waves per
-// SIMD.
+// from the slabs k1 wrote, in k1's split (fp16x3 on v_mfma_f32_32x32x16_f16 with the slabs'
+// layer-wide exponent shifts, or bf16x6 on v_mfma_f32_32x32x16_bf16), two waves per SIMD.
 //
 // Reference: the weight/bias adjoints of nerf.py's reverse pass (reverse_diff.py:492-559;
 // dW_l += A_{l-1}^T G_l, db_l += sum_rows G_l). One workgroup (8 waves)
@@ -24,6 +24,8 @@ typedef float fx4 __attribute__((ext_vector_type(4)));
 typedef float fx16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+typedef _Float16 hf8 __attribute__((ext_vector_type(8)));
+typedef _Float16 hf4 __attribute__((ext_vector_type(4)));
 
 // timing experiments only (wrong results): skip the MFMAs / the slab loads
 #ifndef LNERF_DW16_NOMMA
@@ -35,9 +37,12 @@ typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
 
 constexpr int kThreads = 512;
 constexpr int kRows = 512;                  // A rows [0, 256) and G rows [256, 512) of the image
-constexpr int kPlaneBytes = kRows * 32;     // one plane of a half-block: [row][16 samples] bf16
-constexpr int kImageBytes = 3 * kPlaneBytes;
+constexpr int kPlaneBytes = kRows * 32;     // one plane of a half-block: [row][16 samples] 16-bit
+constexpr int kImageBytes = 3 * kPlaneBytes;   // the largest image (PL = 3)
 constexpr int kLdsBytes = 2 * kImageBytes;  // double-buffered (96 KiB)
+// PL planes per operand: 3 = bf16x6, 2 = fp16x3 (x 2^e = hi + lo, the slab's layer-wide shift)
+template <int PL>
+constexpr int image_bytes() { return PL * kPlaneBytes; }
 
 struct Dw16Args {
     int kt[kMaxLayers], nt[kMaxLayers];
@@ -54,9 +59,20 @@ struct Dw16Args {
     size_t dwp_off[kMaxLayers];
     float* db_part;
     size_t dbp_off[kMaxLayers];
+    const int* smax;            // PL = 2: slab max bits, [l] layer l's input, [L + l] G_l
+    int L;
 };
 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+// the exponent shift e with max 2^e in [2^13, 2^14) from a slab max's bits (0: zero/non-finite)
+__device__ __forceinline__ int shift_of_bits(int bits) {
+    const float m = __int_as_float(bits);
+    if (!(m > 0.0f) || !(m < __builtin_inff())) return 0;
+    int e;
+    (void)__builtin_frexpf(m, &e);
+    return 14 - e;
+}
 
 // The 16 B that thread t loads in round i (0..3) of a half-block: image row r = 128 i + t / 4
 // (rounds 0, 1: A rows; 2, 3: G rows), samples 4 (t % 4) .. +3. A slab block is
@@ -115,25 +131,50 @@ __device__ __forceinline__ void split4(const fx4& x, bf4& h, bf4& m, bf4& lo) {
     }
 }
 
-// Split round i of the thread's values into the plane image (8 B per plane and row).
-__device__ __forceinline__ void write_planes_row(const fx4& v, int i, unsigned char* img) {
-    const int t = threadIdx.x, q = t & 3;
-    const int r = 128 * i + (t >> 2);
-    bf4 h, m, lo;
-    split4(v, h, m, lo);
-    unsigned char* p = img + r * 32 + q * 8;
-    *(bf4*)(p) = h;
-    *(bf4*)(p + kPlaneBytes) = m;
-    *(bf4*)(p + 2 * kPlaneBytes) = lo;
+// x 2^e = hi + lo, round-to-nearest fp16 of each (the remainder is exact in f32)
+__device__ __forceinline__ void split4h(const fx4& x, int e, hf4& h, hf4& lo) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float xs = __builtin_ldexpf(x[k], e);
+        const _Float16 hh = (_Float16)xs;
+        h[k] = hh;
+        lo[k] = (_Float16)(xs - (float)hh);
+    }
 }
 
-__device__ __forceinline__ void write_planes(const Loads& L, unsigned char* img) {
+// Split round i of the thread's values into the plane image (8 B per plane and row); rounds 0, 1
+// are A rows (shift ea), 2, 3 G rows (shift eg).
+template <int PL>
+__device__ __forceinline__ void write_planes_row(const fx4& v, int i, unsigned char* img, int ea, int eg) {
+    const int t = threadIdx.x, q = t & 3;
+    const int r = 128 * i + (t >> 2);
+    unsigned char* p = img + r * 32 + q * 8;
+    if constexpr (PL == 2) {
+        hf4 h, lo;
+        split4h(v, i < 2 ? ea : eg, h, lo);
+        *(hf4*)(p) = h;
+        *(hf4*)(p + kPlaneBytes) = lo;
+    } else {
+        bf4 h, m, lo;
+        split4(v, h, m, lo);
+        *(bf4*)(p) = h;
+        *(bf4*)(p + kPlaneBytes) = m;
+        *(bf4*)(p + 2 * kPlaneBytes) = lo;
+    }
+}
+
+template <int PL>
+__device__ __forceinline__ void write_planes(const Loads& L, unsigned char* img, int ea, int eg) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) write_planes_row(L.v[i], i, img);
+    for (int i = 0; i < 4; ++i) write_planes_row<PL>(L.v[i], i, img, ea, eg);
 }
 
 __device__ __forceinline__ fx16 mfma32(const bf8& a, const bf8& b, fx16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ fx16 mfma32h(const bf8& a, const bf8& b, fx16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(hf8, a), __builtin_bit_cast(hf8, b), c, 0, 0,
+                                                  0);
 }
 
 // The wave's TI x TJ tile block (TI 32-row tiles of A, TJ of G) on one half-block image (per
@@ -141,37 +182,44 @@ __device__ __forceinline__ fx16 mfma32(const bf8& a, const bf8& b, fx16 c) {
 // with the split of the next half-block interleaved (round k beside output column tile k), so
 // the VALU split issues under the MFMAs. Branch-free (ACTIVE is a template parameter; past the
 // split's last half-block the zeroed loads land in the idle image buffer).
-template <int TI, int TJ, bool ACTIVE, bool FULL>
+template <int PL, int TI, int TJ, bool ACTIVE, bool FULL>
 __device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int g0, fx16 (&acc)[TI][TJ],
-                                          const Loads& nl, unsigned char* nxt, const RowMap& m) {
+                                          const Loads& nl, unsigned char* nxt, const RowMap& m, int ea,
+                                          int eg) {
     const int lane = threadIdx.x & 63, fo = (lane & 31) * 32 + (lane >> 5) * 16;
-    bf8 ap[TI][3];
+    bf8 ap[TI][PL];
     if constexpr (ACTIVE) {
 #pragma unroll
         for (int i = 0; i < TI; ++i)
 #pragma unroll
-            for (int p = 0; p < 3; ++p) ap[i][p] = *(const bf8*)(img + p * kPlaneBytes + (a0 + 32 * i) * 32 + fo);
+            for (int p = 0; p < PL; ++p) ap[i][p] = *(const bf8*)(img + p * kPlaneBytes + (a0 + 32 * i) * 32 + fo);
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         // rows past the layer's tiles are never read: skip their split (wave-uniform: a wave's
         // 16 rows of a round lie in one 32-row tile); FULL layers need no branch
-        if (FULL || m.ok[k]) write_planes_row(nl.v[k], k, nxt);
+        if (FULL || m.ok[k]) write_planes_row<PL>(nl.v[k], k, nxt, ea, eg);
         if constexpr (ACTIVE) {
             if (k < TJ) {
                 const int j = k < TJ ? k : 0;
-                bf8 gp[3];
+                bf8 gp[PL];
 #pragma unroll
-                for (int p = 0; p < 3; ++p) gp[p] = *(const bf8*)(img + p * kPlaneBytes + (256 + g0 + 32 * j) * 32 + fo);
+                for (int p = 0; p < PL; ++p) gp[p] = *(const bf8*)(img + p * kPlaneBytes + (256 + g0 + 32 * j) * 32 + fo);
 #pragma unroll
                 for (int i = 0; i < TI; ++i) {
                     fx16 c = acc[i][j];
-                    c = mfma32(ap[i][0], gp[2], c);   // small terms first
-                    c = mfma32(ap[i][1], gp[1], c);
-                    c = mfma32(ap[i][2], gp[0], c);
-                    c = mfma32(ap[i][1], gp[0], c);
-                    c = mfma32(ap[i][0], gp[1], c);
-                    c = mfma32(ap[i][0], gp[0], c);
+                    if constexpr (PL == 2) {
+                        c = mfma32h(ap[i][0], gp[1], c);   // small terms first
+                        c = mfma32h(ap[i][1], gp[0], c);
+                        c = mfma32h(ap[i][0], gp[0], c);
+                    } else {
+                        c = mfma32(ap[i][0], gp[2], c);   // small terms first
+                        c = mfma32(ap[i][1], gp[1], c);
+                        c = mfma32(ap[i][2], gp[0], c);
+                        c = mfma32(ap[i][1], gp[0], c);
+                        c = mfma32(ap[i][0], gp[1], c);
+                        c = mfma32(ap[i][0], gp[0], c);
+                    }
                     acc[i][j] = c;
                 }
             }
@@ -180,17 +228,18 @@ __device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int 
 }
 
 // The half-block loop of one split: L0 holds hb0 (already in the image), L1 hb0 + 1.
-template <int TI, int TJ, bool ACTIVE, bool FULL>
+template <int PL, int TI, int TJ, bool ACTIVE, bool FULL>
 __device__ __forceinline__ void hb_loop(const float* A, const float* G, int kt, int nt, const RowMap& m,
                                         int hb0, int hb1, int a0, int g0, fx16 (&acc)[TI][TJ], Loads& L0,
-                                        Loads& L1, float (&dbs)[2], unsigned char* lds) {
+                                        Loads& L1, float (&dbs)[2], unsigned char* lds, int ea, int eg) {
+    constexpr int kIB = image_bytes<PL>();
     for (int hb = hb0; hb < hb1; ++hb) {
         const int cur = (hb - hb0) & 1;
         // L1 holds hb + 1 (zeros past the end); L0 receives hb + 2
         issue_loads(A, G, kt, nt, m, hb + 2, hb1, L0);
         dbs[0] += (L1.v[2][0] + L1.v[2][1]) + (L1.v[2][2] + L1.v[2][3]);
         dbs[1] += (L1.v[3][0] + L1.v[3][1]) + (L1.v[3][2] + L1.v[3][3]);
-        block_mma<TI, TJ, ACTIVE, FULL>(lds + cur * kImageBytes, a0, g0, acc, L1, lds + (cur ^ 1) * kImageBytes, m);
+        block_mma<PL, TI, TJ, ACTIVE, FULL>(lds + cur * kIB, a0, g0, acc, L1, lds + (cur ^ 1) * kIB, m, ea, eg);
         __syncthreads();
         Loads t = L0;
         L0 = L1;
@@ -200,7 +249,7 @@ __device__ __forceinline__ void hb_loop(const float* A, const float* G, int kt, 
 
 // One split of layer l with TI x TJ tile blocks per wave (the layer's ceil(KT/TI) x ceil(NT/TJ)
 // blocks on waves 0.., at most 8).
-template <int TI, int TJ>
+template <int PL, int TI, int TJ>
 __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsigned char* lds) {
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
     const int KT = a.kt[l], NT = a.nt[l];
@@ -223,20 +272,23 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
     const float* A = a.act + a.a_off[l];
     const float* G = a.grad + a.g_off[l];
     const RowMap m = row_map(KT, NT);
+    // PL = 2: the layer-wide exponent shifts of the A_{l-1} and G_l slabs (k1's slab maxima); the
+    // partials are shifted back by -(ea + eg) (exact)
+    const int ea = PL == 2 ? shift_of_bits(a.smax[l]) : 0, eg = PL == 2 ? shift_of_bits(a.smax[a.L + l]) : 0;
     Loads L0, L1;
     issue_loads(A, G, KT, NT, m, hb0, hb1, L0);
     issue_loads(A, G, KT, NT, m, hb0 + 1, hb1, L1);
     if (hb0 < hb1) {
         dbs[0] += (L0.v[2][0] + L0.v[2][1]) + (L0.v[2][2] + L0.v[2][3]);
         dbs[1] += (L0.v[3][0] + L0.v[3][1]) + (L0.v[3][2] + L0.v[3][3]);
-        write_planes(L0, lds);
+        write_planes<PL>(L0, lds, ea, eg);
     }
     __syncthreads();
     const bool full = KT == 8 && NT == 8;
-    if (active && full) hb_loop<TI, TJ, true, true>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds);
-    else if (active) hb_loop<TI, TJ, true, false>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds);
-    else if (full) hb_loop<TI, TJ, false, true>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds);
-    else hb_loop<TI, TJ, false, false>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds);
+    if (active && full) hb_loop<PL, TI, TJ, true, true>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, ea, eg);
+    else if (active) hb_loop<PL, TI, TJ, true, false>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, ea, eg);
+    else if (full) hb_loop<PL, TI, TJ, false, true>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, ea, eg);
+    else hb_loop<PL, TI, TJ, false, false>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, ea, eg);
 
     // partial [split][k][j], k < KT*32, j < NT*32 (32x32 C/D layout: row (r&3)+8(r>>2)+4h, col l&31)
     if (active) {
@@ -251,7 +303,8 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
                         const int k = kb + (r & 3) + 8 * (r >> 2) + 4 * h;
-                        part[(size_t)k * ncol + jb + (lane & 31)] = acc[i][j][r];
+                        part[(size_t)k * ncol + jb + (lane & 31)] =
+                            PL == 2 ? __builtin_ldexpf(acc[i][j][r], -(ea + eg)) : acc[i][j][r];
                     }
                 }
             }
@@ -275,16 +328,33 @@ __host__ __device__ __forceinline__ int dw_shape(int kt, int nt) {
     return 2;
 }
 
+template <int PL>
 __global__ void __launch_bounds__(kThreads, 1) dw16_kernel(Dw16Args a) {
-    __shared__ __attribute__((aligned(16))) unsigned char lds[kLdsBytes];
+    __shared__ __attribute__((aligned(16))) unsigned char lds[2 * image_bytes<PL>()];
     int li = 0;
     while (li + 1 < a.nl && (int)blockIdx.x >= a.wg_off[li + 1]) ++li;
     const int l = a.lid[li], sp = blockIdx.x - a.wg_off[li];
     switch (dw_shape(a.kt[l], a.nt[l])) {
-        case 0: dw_split<1, 1>(a, l, sp, lds); break;
-        case 1: dw_split<1, 2>(a, l, sp, lds); break;
-        default: dw_split<2, 4>(a, l, sp, lds); break;
+        case 0: dw_split<PL, 1, 1>(a, l, sp, lds); break;
+        case 1: dw_split<PL, 1, 2>(a, l, sp, lds); break;
+        default: dw_split<PL, 2, 4>(a, l, sp, lds); break;
     }
+}
+
+// PL = 2: slab blockIdx.x's layer-wide max from k1's per-wave maxima (n per slab), as the bits of
+// a non-negative float in smax[slab]
+__global__ void slab_max_reduce_kernel(const float* __restrict__ part, int n, int* __restrict__ smax) {
+    const float* q = part + (size_t)blockIdx.x * n;
+    float m = 0.0f;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) m = fmaxf(m, q[i]);
+    __shared__ float red[256];
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + w]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) smax[blockIdx.x] = __float_as_int(red[0]);
 }
 
 }  // namespace
@@ -309,7 +379,13 @@ void dw16_launch(const FusedPlan& p, hipStream_t s) {
     a.blocks = p.blocks;
     a.dw_part = p.dw_part;
     a.db_part = p.db_part;
-    dw16_kernel<<<p.dw_grid, kThreads, 0, s>>>(a);
+    a.smax = p.smax16;
+    a.L = p.L;
+    if (p.x6 == 2) {
+        slab_max_reduce_kernel<<<2 * p.L, 256, 0, s>>>(p.smax_part, p.num_wg * 8, p.smax16);
+        dw16_kernel<2><<<p.dw_grid, kThreads, 0, s>>>(a);
+    }
+    else dw16_kernel<3><<<p.dw_grid, kThreads, 0, s>>>(a);
 }
 
 }  // namespace lnerf

@@ -1613,7 +1613,8 @@ size_t fused_workspace_bytes(const lnerf_mlp& m, int rays, int S, bool train) {
                align_up(y.act_total, 64) + align_up(y.grad_total, 64) +
                align_up((size_t)y.num_wg, 64) + align_up(y.dwp_total, 64) + align_up(y.dbp_total, 64) +
                64 + align_up((y.w16_total + 1) / 2, 64) + align_up(y.b16_total, 64) +
-               align_up(y.mask_total * 2, 64) + 64;   // + the fp16x3 weight exponent shifts
+               align_up(y.mask_total * 2, 64) + 64 +   // + the fp16x3 weight/slab maxima
+               (train ? align_up((size_t)2 * m.num_layers * y.num_wg * 8, 64) : 0);
     return f * sizeof(float);
 }
 
@@ -1697,7 +1698,10 @@ void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws
     p.mask_g = (unsigned long long*)(base + off);
     off += align_up(y.mask_total * 2, 64);
     p.wexp16 = (int*)(base + off);
+    p.smax16 = p.wexp16 + kMaxLayers;
     off += 64;
+    p.smax_part = base + off;
+    if (train) off += align_up((size_t)2 * p.L * y.num_wg * 8, 64);
 
     p.x_off = y.x_off;
     p.ht16 = y.ht16;

@@ -159,7 +159,9 @@ struct FusedPlan {
     float* b16;                          // [L][256] zero-padded biases
     unsigned long long* mask_g;          // [num_wg][L-1][8 waves][64 lanes] ReLU mask bits
     int dw16;                            // 1: dW by dw16_kernel (lnerf_dw16.hip), one partial per split
-    int* wexp16;                         // x6 = 2: per-layer exponent shift of the fp16 weight planes
+    int* wexp16;                         // x6 = 2: per-layer max|W| bits (fp16 weight plane shifts)
+    int* smax16;                         // x6 = 2: per-slab max bits ([l] input of layer l, [L+l] G_l)
+    float* smax_part;                    // x6 = 2: k1's per-wave slab maxima [2L][num_wg * 8]
 };
 
 bool fused_supported(const lnerf_mlp& mlp, int rays, int S, int input_mode, const char** why);

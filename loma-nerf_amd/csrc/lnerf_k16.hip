@@ -111,6 +111,8 @@ struct K16Args {
     int want_grad;
     int planes;
     const int* wexp;   // PL = 2: per-layer max|W| bits of the packed fp16 weight planes (wshift_of)
+    float* smax;       // PL = 2, training: per-wave slab maxima [2L][num_wg * 8]: slab l the input
+                       // of layer l (X, A_l-1), slab L + l G_l
 };
 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
@@ -408,22 +410,37 @@ __device__ __forceinline__ void k16_pass_n(const K16Args& a, int ks, int& ci, un
     else k16_pass<16, PL>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
 }
 
-// PL = 2: the per-sample exponent shift of a pass's input (lanes n, n + 16, n + 32, n + 48 hold
-// sample n's features): max|x| 2^ex in [2^13, 2^14); 0 for an all-zero (or non-finite) sample.
+// PL = 2: the per-sample max|x| of a pass's input (lanes n, n + 16, n + 32, n + 48 hold sample
+// n's features), the basis of its exponent shift.
 template <int PL>
-__device__ __forceinline__ int sample_shift(const fx4 (&in)[kMaxT]) {
-    if constexpr (PL != 2) return 0;
+__device__ __forceinline__ float sample_max(const fx4 (&in)[kMaxT]) {
+    if constexpr (PL != 2) return 0.0f;
     float m = 0.0f;
 #pragma unroll
     for (int o = 0; o < kMaxT; ++o)
 #pragma unroll
         for (int i = 0; i < 4; ++i) m = __builtin_fmaxf(m, __builtin_fabsf(in[o][i]));
     m = __builtin_fmaxf(m, __shfl_xor(m, 16));
-    m = __builtin_fmaxf(m, __shfl_xor(m, 32));
+    return __builtin_fmaxf(m, __shfl_xor(m, 32));
+}
+
+// the exponent shift ex with m 2^ex in [2^13, 2^14); 0 for m = 0 (or non-finite)
+__device__ __forceinline__ int shift_of(float m) {
     if (!(m > 0.0f) || !(m < __builtin_inff())) return 0;
     int e;
     (void)__builtin_frexpf(m, &e);   // m = f 2^e, f in [0.5, 1)
     return 14 - e;
+}
+
+// PL = 2, training: the wave's max of a slab, one plain store per wave and slab into
+// smax_part[slab][global wave] (slab_max_reduce folds them into dw16's layer-wide exponent
+// shifts; an atomic per wave on 2L shared words measured 2.2x slower for the whole kernel).
+// Issued before the pass's first DMA, so it is older than every piece a dma_barrier waits for.
+__device__ __forceinline__ void slab_max(float* part, int slab, float m) {
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) m = __builtin_fmaxf(m, __shfl_xor(m, d));
+    if ((threadIdx.x & 63) == 0)
+        part[(size_t)slab * gridDim.x * kWaves + blockIdx.x * kWaves + (threadIdx.x >> 6)] = m;
 }
 
 // The layer's biases in the accumulator layout (fx4 = 4 consecutive features of a lane group),
@@ -548,7 +565,9 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
                                 half * 512;
         zero_tiles(out);
         const unsigned bl = lds_addr(bias_ring + (l % 3) * 256) + g * 16;
-        const int ex = sample_shift<PL>(act);
+        const float xm = sample_max<PL>(act);
+        if (PL == 2 && st) slab_max(a.smax, l, xm);
+        const int ex = shift_of(xm);
         const int sh = unscale(l, ex);
         if (l < a.L - 1) {
             PROF_T(t_f);
@@ -611,7 +630,9 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
         float* slab = a.grad + a.grad_off[l] + blk * (size_t)(a.nt[l] * 1024) + half * 512;
         PROF_T(t_b);
         const unsigned long long mb = mask_w[(size_t)(l - 1) * kWaves * 64];   // in flight over the pass
-        const int ex = sample_shift<PL>(act);
+        const float xm = sample_max<PL>(act);
+        if (PL == 2) slab_max(a.smax, a.L + l, xm);
+        const int ex = shift_of(xm);
         const int sh = unscale(l, ex);
         k16_pass<HT, PL>(a, a.ks_b[l], ci, ring, bias_ring, act, out, slab, ex);
         PROF_ADD(kPfBwd, t_b);
@@ -630,7 +651,9 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
     if (a.d_x) {
         // d_layer_input = G_0 W_0^T (ENCODED mode); the pass also writes G_0's slab
         zero_tiles(out);
-        const int ex = sample_shift<PL>(act);
+        const float xm = sample_max<PL>(act);
+        if (PL == 2) slab_max(a.smax, a.L, xm);
+        const int ex = shift_of(xm);
         const int sh = unscale(0, ex);
         k16_pass_n<PL>(a, a.ks_b[0], ci, ring, bias_ring, a.to_b[0], act, out, g0, ex);
         if (valid) {
@@ -645,6 +668,7 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
                 }
         }
     } else {
+        if (PL == 2) slab_max(a.smax, a.L, sample_max<PL>(act));
 #pragma unroll
         for (int s = 0; s < 8; ++s)
             if (s < a.ks_b[0]) store_slab_step(g0 + s * 1024, act[2 * s], act[2 * s + 1]);
@@ -815,6 +839,7 @@ void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lner
     a.want_grad = want_grad ? 1 : 0;
     a.planes = p.x6;
     a.wexp = p.wexp16;
+    a.smax = p.smax_part;
     // the chunk stream: forward 0..L-1, backward L-1..1 (training), backward 0 (d_x)
     {
         int ci = 0;

@@ -245,6 +245,19 @@ __device__ __forceinline__ int wshift_of(int maxbits) {
     return 14 - e;
 }
 
+// The same split for a pair (x0, x1) packed as two f16 per register, with v_fma_mix: hi =
+// round_f16(x sc) and lo = round_f16(x sc - hi) are fused multiply-adds with one rounding to f16
+// (x sc is exact, sc a power of two; x sc - hi is exact), two instructions per value instead of
+// scale, convert, widen, subtract and convert.
+__device__ __forceinline__ void split_h2(float x0, float x1, float sc, unsigned& hi, unsigned& lo) {
+    asm("v_fma_mixlo_f16 %0, %1, %2, 0 op_sel_hi:[0,0,0]" : "=&v"(hi) : "v"(x0), "v"(sc));
+    asm("v_fma_mixhi_f16 %0, %1, %2, 0 op_sel_hi:[0,0,0]" : "+v"(hi) : "v"(x1), "v"(sc));
+    asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel:[0,0,0] op_sel_hi:[0,0,1]"
+        : "=&v"(lo) : "v"(x0), "v"(sc), "v"(hi));
+    asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+        : "+v"(lo) : "v"(x1), "v"(sc), "v"(hi));
+}
+
 // x = hi + mid + lo (round-to-nearest bf16 of each remainder; every remainder is exact in f32)
 __device__ __forceinline__ void split_x(float x, __bf16& h, __bf16& m, __bf16& l) {
     h = (__bf16)x;
@@ -288,10 +301,18 @@ __device__ __forceinline__ void lgkm_wait(bf8 (&w)[3]) {
 
 constexpr int kDist = 2;   // weight tiles read ahead of the one the MFMAs consume
 
+// timing experiments only (wrong results): read one plane per tile / skip the operand split
+#ifndef LNERF_K16_HALFLDS
+#define LNERF_K16_HALFLDS 0
+#endif
+#ifndef LNERF_K16_NOSPLIT
+#define LNERF_K16_NOSPLIT 0
+#endif
 template <int PL, int O>
 __device__ __forceinline__ void read_tile(unsigned base, bf8 (&w)[3]) {
     w[0] = ds_read_at<(O * PL + 0) * 1024>(base);
-    if constexpr (PL >= 2) w[1] = ds_read_at<(O * PL + 1) * 1024>(base);
+    if constexpr (PL >= 2 && LNERF_K16_HALFLDS) w[1] = w[0];
+    else if constexpr (PL >= 2) w[1] = ds_read_at<(O * PL + 1) * 1024>(base);
     if constexpr (PL == 3) w[2] = ds_read_at<(O * PL + 2) * 1024>(base);
 }
 
@@ -303,7 +324,7 @@ __device__ __forceinline__ void tile_step(unsigned base, bf8 (&w)[kDist + 1][3],
     if constexpr (O + kDist < NTO) read_tile<PL, O + kDist>(base, w[(O + kDist) % (kDist + 1)]);
     constexpr int ahead = (NTO - 1 - O) < kDist ? (NTO - 1 - O) : kDist;
     bf8(&c)[3] = w[O % (kDist + 1)];
-    lgkm_wait<ahead * PL>(c);
+    lgkm_wait<ahead * (LNERF_K16_HALFLDS && PL == 2 ? 1 : PL)>(c);
     fx4 acc = out[O];
     if constexpr (PL == 2) {
         // fp16x3: small terms first (w_hi x_lo, w_lo x_hi), then w_hi x_hi; (bh, bm) = (x_hi, x_lo)
@@ -331,6 +352,44 @@ __device__ __forceinline__ void tile_steps(std::integer_sequence<int, O...>, uns
     (tile_step<NTO, PL, B + O>(base, w, bh, bm, bl, out), ...);
 }
 
+// The B operand planes of k-step s (the lane's 8 input features phi(s, g, 0..7) of its sample):
+// bf16x6 hi/mid/lo, fp16x3 hi/lo (x 2^ex), or plain bf16.
+template <int PL>
+__device__ __forceinline__ void make_b(const fx4 (&in)[kMaxT], int s, int ex, bf8& bh, bf8& bm, bf8& bl) {
+    if constexpr (PL == 2 && !LNERF_K16_NOSPLIT) {
+        typedef unsigned u4 __attribute__((ext_vector_type(4)));
+        u4 hv, lv;
+        const float sc = __builtin_ldexpf(1.0f, ex);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const fx4& t = in[2 * s + (q >> 1)];
+            unsigned h2, l2;
+            split_h2(t[2 * (q & 1)], t[2 * (q & 1) + 1], sc, h2, l2);
+            hv[q] = h2;
+            lv[q] = l2;
+        }
+        bh = __builtin_bit_cast(bf8, hv);
+        bm = __builtin_bit_cast(bf8, lv);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float x = j < 4 ? in[2 * s][j] : in[2 * s + 1][j - 4];
+            if (PL == 3) {
+                __bf16 h, m, l;
+                split_x(x, h, m, l);
+                bh[j] = h;
+                bm[j] = m;
+                bl[j] = l;
+            } else if (PL == 2) {   // LNERF_K16_NOSPLIT timing experiment
+                bh[j] = __builtin_bit_cast(__bf16, (_Float16)x);
+                bm[j] = bh[j];
+            } else {
+                bh[j] = (__bf16)x;
+            }
+        }
+    }
+}
+
 // One pass (a layer's forward or backward MMA): out[o] += sum over the pass's k-steps of
 // Wpack[s][o] (x) in[2s..2s+1], NTO output tiles. Chunk ci is read from ring slot ci % kSlots
 // while chunk ci+kAhead (issued here) lands. `slab` (nullable)
@@ -341,6 +400,8 @@ __device__ __forceinline__ void k16_pass(const K16Args& a, int ks, int& ci, unsi
                                          float* __restrict__ slab, int ex = 0) {
     const int lane = threadIdx.x & 63;
     constexpr int kSB = slot_bytes<PL>();
+    bf8 bh = {}, bm = {}, bl = {};
+    make_b<PL>(in, 0, ex, bh, bm, bl);
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
         if (s < ks) {
@@ -352,6 +413,8 @@ __device__ __forceinline__ void k16_pass(const K16Args& a, int ks, int& ci, unsi
             // operations younger than them stay in flight -- this k-step's 8 slab stores and
             // (kAhead = 2) chunk ci+2's pieces. A wave that issues no DMA does not wait at all
             // (its slab stores need no completion before the barrier).
+            // (register staging -- 16-B loads after the prologue, ds_write_b128 before the barrier
+            // -- measured slower: 1.52 vs 1.40 ms)
             const int issued = (LNERF_K16_NODMA && ci >= 2)
                                    ? 0
                                    : dma_chunk(a, chunk_at(a, ci + kAhead),
@@ -368,32 +431,19 @@ __device__ __forceinline__ void k16_pass(const K16Args& a, int ks, int& ci, unsi
             // (an LDS-transposed form -- 8 ds_write_b32 + 2 ds_read_b128 + 2 dwordx4 stores --
             // measured slower: 2.13-2.18 vs 2.02-2.03 ms)
             if (slab && !LNERF_K16_NOSTORE) store_slab_step(slab + s * 1024, in[2 * s], in[2 * s + 1]);
-            bf8 bh, bm = {}, bl = {};
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float x = j < 4 ? in[2 * s][j] : in[2 * s + 1][j - 4];
-                if (PL == 3) {
-                    __bf16 h, m, l;
-                    split_x(x, h, m, l);
-                    bh[j] = h;
-                    bm[j] = m;
-                    bl[j] = l;
-                } else if (PL == 2) {
-                    _Float16 h, l;
-                    split_h(__builtin_ldexpf(x, ex), h, l);
-                    bh[j] = __builtin_bit_cast(__bf16, h);
-                    bm[j] = __builtin_bit_cast(__bf16, l);
-                } else {
-                    bh[j] = (__bf16)x;
-                }
-            }
             static_assert(kDist == 2, "the prologue reads kDist tiles");
-            // first half of the output tiles, [late waves: barrier], second half, [early: barrier]
+            // first half of the output tiles, [late waves: barrier], the next k-step's operand
+            // split (off the next prologue's critical path), second half, [early: barrier]
             constexpr int H = (NTO + 1) / 2;
             tile_steps<NTO, PL, 0>(std::make_integer_sequence<int, H>{}, base, w, bh, bm, bl, out);
             if (late) dma_barrier(pending);
+            bf8 nh = {}, nm = {}, nl = {};
+            if (s + 1 < ks) make_b<PL>(in, s + 1 < 8 ? s + 1 : 0, ex, nh, nm, nl);
             tile_steps<NTO, PL, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, bh, bm, bl, out);
             if (!late) dma_barrier(pending);
+            bh = nh;
+            bm = nm;
+            bl = nl;
             ++ci;
         }
     }

@@ -79,20 +79,22 @@ __device__ __forceinline__ int shift_of_bits(int bits) {
 // [tile][half][32 rows][16 samples]; a half-block is one half of one 32-sample block. The
 // per-thread part of the offset is fixed (RowMap), the half-block part is wave-uniform.
 struct RowMap {
-    int off[4];      // float offset inside a half-block of the slab
-    bool ok[4];      // the row exists in this layer (else the value is zero)
+    int lane;        // per-thread float offset inside a tile's half: row (t/4) % 32, samples 4 (t % 4)
+    int tile[4];     // wave-uniform: the 32-row tile of round i (tile 0 for rows past the layer)
+    bool ok[4];      // wave-uniform: the row exists in this layer (else it is never split)
 };
 
 __device__ __forceinline__ RowMap row_map(int kt, int nt) {
     RowMap m;
-    const int t = threadIdx.x, q = t & 3;
+    const int t = threadIdx.x;
+    m.lane = ((t >> 2) & 31) * 16 + 4 * (t & 3);
+    // a round's 16 rows of a wave lie in one tile: tile = (128 (i & 1) + t / 4) / 32 = 4 (i & 1) + wave / 2
+    const int w2 = wave_id() >> 1;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int rr = 128 * (i & 1) + (t >> 2);   // row within A (i < 2) or G (i >= 2)
-        const int tiles = i < 2 ? kt : nt;
-        m.ok[i] = (rr >> 5) < tiles;
-        const int rc = m.ok[i] ? rr : (rr & 31);   // a valid row of tile 0 past the layer's tiles
-        m.off[i] = (rc >> 5) * 1024 + (rc & 31) * 16 + 4 * q;
+        const int tl = 4 * (i & 1) + w2;
+        m.ok[i] = tl < (i < 2 ? kt : nt);
+        m.tile[i] = m.ok[i] ? tl : 0;
     }
     return m;
 }
@@ -101,8 +103,9 @@ struct Loads {
     fx4 v[4];
 };
 
-// Always four loads (rows past the layer's tiles and half-blocks past the split read a valid
-// address and are zeroed), so the compiler's vmcnt for them is exact.
+// Always four loads from valid addresses and no select on the data (nothing waits for it before
+// its use): rows past the layer's tiles are never split, half-blocks past the split land in the
+// idle image and add nothing to db (the callers' hb < hb1 guards).
 __device__ __forceinline__ void issue_loads(const float* A, const float* G, int kt, int nt, const RowMap& m,
                                             int hb, int hb_end, Loads& L) {
     const bool in = hb < hb_end;
@@ -112,9 +115,8 @@ __device__ __forceinline__ void issue_loads(const float* A, const float* G, int 
     const float* pg = G + (size_t)blk * nt * 1024 + half * 512;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const fx4* p = (const fx4*)((i < 2 ? pa : pg) + m.off[i]);
-        const fx4 v = LNERF_DW16_NOLOAD ? fx4{1.0f, 2.0f, 3.0f, (float)i} : __builtin_nontemporal_load(p);
-        L.v[i] = (m.ok[i] && in) ? v : fx4{0.0f, 0.0f, 0.0f, 0.0f};
+        const fx4* p = (const fx4*)((i < 2 ? pa : pg) + m.tile[i] * 1024 + m.lane);
+        L.v[i] = LNERF_DW16_NOLOAD ? fx4{1.0f, 2.0f, 3.0f, (float)i} : __builtin_nontemporal_load(p);
     }
 }
 
@@ -131,15 +133,15 @@ __device__ __forceinline__ void split4(const fx4& x, bf4& h, bf4& m, bf4& lo) {
     }
 }
 
-// x 2^e = hi + lo, round-to-nearest fp16 of each (the remainder is exact in f32)
-__device__ __forceinline__ void split4h(const fx4& x, int e, hf4& h, hf4& lo) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const float xs = __builtin_ldexpf(x[k], e);
-        const _Float16 hh = (_Float16)xs;
-        h[k] = hh;
-        lo[k] = (_Float16)(xs - (float)hh);
-    }
+// The pair (x0, x1) as packed f16 hi = round(x sc), lo = round(x sc - hi) by v_fma_mix (one
+// rounding each; x sc and x sc - hi are exact): two instructions per value.
+__device__ __forceinline__ void split_h2(float x0, float x1, float sc, unsigned& hi, unsigned& lo) {
+    asm("v_fma_mixlo_f16 %0, %1, %2, 0 op_sel_hi:[0,0,0]" : "=&v"(hi) : "v"(x0), "v"(sc));
+    asm("v_fma_mixhi_f16 %0, %1, %2, 0 op_sel_hi:[0,0,0]" : "+v"(hi) : "v"(x1), "v"(sc));
+    asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel:[0,0,0] op_sel_hi:[0,0,1]"
+        : "=&v"(lo) : "v"(x0), "v"(sc), "v"(hi));
+    asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+        : "+v"(lo) : "v"(x1), "v"(sc), "v"(hi));
 }
 
 // Split round i of the thread's values into the plane image (8 B per plane and row); rounds 0, 1
@@ -150,10 +152,13 @@ __device__ __forceinline__ void write_planes_row(const fx4& v, int i, unsigned c
     const int r = 128 * i + (t >> 2);
     unsigned char* p = img + r * 32 + q * 8;
     if constexpr (PL == 2) {
-        hf4 h, lo;
-        split4h(v, i < 2 ? ea : eg, h, lo);
-        *(hf4*)(p) = h;
-        *(hf4*)(p + kPlaneBytes) = lo;
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+        const float sc = __builtin_ldexpf(1.0f, i < 2 ? ea : eg);
+        unsigned h0, l0, h1, l1;
+        split_h2(v[0], v[1], sc, h0, l0);
+        split_h2(v[2], v[3], sc, h1, l1);
+        *(u2*)(p) = u2{h0, h1};
+        *(u2*)(p + kPlaneBytes) = u2{l0, l1};
     } else {
         bf4 h, m, lo;
         split4(v, h, m, lo);
@@ -235,16 +240,58 @@ __device__ __forceinline__ void hb_loop(const float* A, const float* G, int kt, 
     constexpr int kIB = image_bytes<PL>();
     for (int hb = hb0; hb < hb1; ++hb) {
         const int cur = (hb - hb0) & 1;
-        // L1 holds hb + 1 (zeros past the end); L0 receives hb + 2
+        // L1 holds hb + 1; L0 receives hb + 2
         issue_loads(A, G, kt, nt, m, hb + 2, hb1, L0);
-        dbs[0] += (L1.v[2][0] + L1.v[2][1]) + (L1.v[2][2] + L1.v[2][3]);
-        dbs[1] += (L1.v[3][0] + L1.v[3][1]) + (L1.v[3][2] + L1.v[3][3]);
+        if (hb + 1 < hb1) {
+            dbs[0] += (L1.v[2][0] + L1.v[2][1]) + (L1.v[2][2] + L1.v[2][3]);
+            dbs[1] += (L1.v[3][0] + L1.v[3][1]) + (L1.v[3][2] + L1.v[3][3]);
+        }
         block_mma<PL, TI, TJ, ACTIVE, FULL>(lds + cur * kIB, a0, g0, acc, L1, lds + (cur ^ 1) * kIB, m, ea, eg);
         __syncthreads();
         Loads t = L0;
         L0 = L1;
         L1 = t;
     }
+}
+
+// Three half-blocks in flight (LNERF_DW16_DEPTH=3): step I of a 3-step rotation over the load
+// register sets (images alternate at run time). Entering half-block hb: its planes are in image
+// (hb - hb0) & 1, the set after I holds hb + 1 (split now into the other image), the one after
+// that hb + 2 (in flight) and set I is free: it receives hb + 3.
+#ifndef LNERF_DW16_DEPTH
+#define LNERF_DW16_DEPTH 3
+#endif
+template <int PL, int TI, int TJ, bool ACTIVE, bool FULL, int I>
+__device__ __forceinline__ void hb_step3(const float* A, const float* G, int kt, int nt, const RowMap& m, int hb,
+                                         int hb0, int hb1, int a0, int g0, fx16 (&acc)[TI][TJ], Loads& L0,
+                                         Loads& L1, Loads& L2, float (&dbs)[2], unsigned char* lds, int ea,
+                                         int eg) {
+    constexpr int kIB = image_bytes<PL>();
+    Loads& fr = I == 0 ? L0 : I == 1 ? L1 : L2;
+    const Loads& nx = I == 0 ? L1 : I == 1 ? L2 : L0;
+    issue_loads(A, G, kt, nt, m, hb + 3, hb1, fr);
+    if (hb + 1 < hb1) {
+        dbs[0] += (nx.v[2][0] + nx.v[2][1]) + (nx.v[2][2] + nx.v[2][3]);
+        dbs[1] += (nx.v[3][0] + nx.v[3][1]) + (nx.v[3][2] + nx.v[3][3]);
+    }
+    const int cur = (hb - hb0) & 1;
+    block_mma<PL, TI, TJ, ACTIVE, FULL>(lds + cur * kIB, a0, g0, acc, nx, lds + (cur ^ 1) * kIB, m, ea, eg);
+    __syncthreads();
+}
+
+template <int PL, int TI, int TJ, bool ACTIVE, bool FULL>
+__device__ __forceinline__ void hb_loop3(const float* A, const float* G, int kt, int nt, const RowMap& m,
+                                         int hb0, int hb1, int a0, int g0, fx16 (&acc)[TI][TJ], Loads& L0,
+                                         Loads& L1, Loads& L2, float (&dbs)[2], unsigned char* lds, int ea,
+                                         int eg) {
+    int hb = hb0;
+    for (; hb + 3 <= hb1; hb += 3) {
+        hb_step3<PL, TI, TJ, ACTIVE, FULL, 0>(A, G, kt, nt, m, hb, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, ea, eg);
+        hb_step3<PL, TI, TJ, ACTIVE, FULL, 1>(A, G, kt, nt, m, hb + 1, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, ea, eg);
+        hb_step3<PL, TI, TJ, ACTIVE, FULL, 2>(A, G, kt, nt, m, hb + 2, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, ea, eg);
+    }
+    if (hb < hb1) hb_step3<PL, TI, TJ, ACTIVE, FULL, 0>(A, G, kt, nt, m, hb, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, ea, eg);
+    if (hb + 1 < hb1) hb_step3<PL, TI, TJ, ACTIVE, FULL, 1>(A, G, kt, nt, m, hb + 1, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, ea, eg);
 }
 
 // One split of layer l with TI x TJ tile blocks per wave (the layer's ceil(KT/TI) x ceil(NT/TJ)
@@ -275,20 +322,37 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
     // PL = 2: the layer-wide exponent shifts of the A_{l-1} and G_l slabs (k1's slab maxima); the
     // partials are shifted back by -(ea + eg) (exact)
     const int ea = PL == 2 ? shift_of_bits(a.smax[l]) : 0, eg = PL == 2 ? shift_of_bits(a.smax[a.L + l]) : 0;
-    Loads L0, L1;
-    issue_loads(A, G, KT, NT, m, hb0, hb1, L0);
-    issue_loads(A, G, KT, NT, m, hb0 + 1, hb1, L1);
-    if (hb0 < hb1) {
-        dbs[0] += (L0.v[2][0] + L0.v[2][1]) + (L0.v[2][2] + L0.v[2][3]);
-        dbs[1] += (L0.v[3][0] + L0.v[3][1]) + (L0.v[3][2] + L0.v[3][3]);
-        write_planes<PL>(L0, lds, ea, eg);
-    }
-    __syncthreads();
     const bool full = KT == 8 && NT == 8;
-    if (active && full) hb_loop<PL, TI, TJ, true, true>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, ea, eg);
-    else if (active) hb_loop<PL, TI, TJ, true, false>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, ea, eg);
-    else if (full) hb_loop<PL, TI, TJ, false, true>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, ea, eg);
-    else hb_loop<PL, TI, TJ, false, false>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, ea, eg);
+    if constexpr (LNERF_DW16_DEPTH == 3) {
+        Loads L0, L1, L2;
+        issue_loads(A, G, KT, NT, m, hb0, hb1, L0);
+        issue_loads(A, G, KT, NT, m, hb0 + 1, hb1, L1);
+        issue_loads(A, G, KT, NT, m, hb0 + 2, hb1, L2);
+        if (hb0 < hb1) {
+            dbs[0] += (L0.v[2][0] + L0.v[2][1]) + (L0.v[2][2] + L0.v[2][3]);
+            dbs[1] += (L0.v[3][0] + L0.v[3][1]) + (L0.v[3][2] + L0.v[3][3]);
+            write_planes<PL>(L0, lds, ea, eg);
+        }
+        __syncthreads();
+        if (active && full) hb_loop3<PL, TI, TJ, true, true>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, ea, eg);
+        else if (active) hb_loop3<PL, TI, TJ, true, false>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, ea, eg);
+        else if (full) hb_loop3<PL, TI, TJ, false, true>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, ea, eg);
+        else hb_loop3<PL, TI, TJ, false, false>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, ea, eg);
+    } else {
+        Loads L0, L1;
+        issue_loads(A, G, KT, NT, m, hb0, hb1, L0);
+        issue_loads(A, G, KT, NT, m, hb0 + 1, hb1, L1);
+        if (hb0 < hb1) {
+            dbs[0] += (L0.v[2][0] + L0.v[2][1]) + (L0.v[2][2] + L0.v[2][3]);
+            dbs[1] += (L0.v[3][0] + L0.v[3][1]) + (L0.v[3][2] + L0.v[3][3]);
+            write_planes<PL>(L0, lds, ea, eg);
+        }
+        __syncthreads();
+        if (active && full) hb_loop<PL, TI, TJ, true, true>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, ea, eg);
+        else if (active) hb_loop<PL, TI, TJ, true, false>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, ea, eg);
+        else if (full) hb_loop<PL, TI, TJ, false, true>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, ea, eg);
+        else hb_loop<PL, TI, TJ, false, false>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, ea, eg);
+    }
 
     // partial [split][k][j], k < KT*32, j < NT*32 (32x32 C/D layout: row (r&3)+8(r>>2)+4h, col l&31)
     if (active) {

@@ -299,10 +299,11 @@ def main():
             fus_ms = kt["fused"]
             peak = (PEAK_FP32_TFLOPS if args.mfma_f32 else PEAK_X6_TFLOPS if args.x6_train
                     else PEAK_F16X3_TFLOPS)
-            # the fused kernel the engine ran: k16 (wave pairs, default for the bf16 planes) or
-            # the one-wave-per-SIMD kernel (exact f32 MFMA, or LNERF_K16=0)
-            k1 = ("fused_fwd_bwd_kernel" if args.mfma_f32 or os.environ.get("LNERF_K16") == "0"
-                  else "k16_fwd_bwd_kernel")
+            # the fused kernel the engine ran: kact (LDS-resident activations, the fp16x3
+            # default), k16 (wave pairs) or the one-wave-per-SIMD kernel (exact f32 MFMA)
+            lp = eng.last_path()
+            k1 = ("kact_fwd_bwd_kernel" if lp["kact"] else "k16_fwd_bwd_kernel" if lp["k16"]
+                  else "fused_fwd_bwd_kernel")
             out["roofline"] = {"bound": "mfma", "kernel": k1,
                                "achieved": fused_flops / (fus_ms / 1e3) / 1e12,
                                "peak": peak, "unit": "TFLOP/s",

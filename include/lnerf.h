@@ -194,7 +194,8 @@ enum {
     LNERF_PATH_GENERIC = 1,   /* the loma-order stage-by-stage kernels                        */
     LNERF_PATH_FUSED = 2,     /* the fused MFMA step (any kernel pair below)                  */
     LNERF_PATH_K16 = 4,       /* fused kernel on wave pairs (k16_fwd_bwd_kernel)              */
-    LNERF_PATH_DW16 = 8       /* dW kernel on wave pairs (dw16_kernel)                        */
+    LNERF_PATH_DW16 = 8,      /* dW kernel on wave pairs (dw16_kernel)                        */
+    LNERF_PATH_KACT = 16      /* fused kernel with LDS-resident activations (kact_fwd_bwd_kernel) */
 };
 int lnerf_ctx_last_path(lnerf_ctx* ctx);
 

@@ -592,8 +592,8 @@ struct lnerf_ctx {
 };
 
 static int path_bits(const FusedPlan& p, bool train) {
-    return LNERF_PATH_FUSED | (p.k16 ? LNERF_PATH_K16 : 0) | (train && p.dw16 ? LNERF_PATH_DW16 : 0) |
-           (p.x6 << 8);
+    return LNERF_PATH_FUSED | (p.kact ? LNERF_PATH_KACT : p.k16 ? LNERF_PATH_K16 : 0) |
+           (train && p.dw16 ? LNERF_PATH_DW16 : 0) | (p.x6 << 8);
 }
 
 extern "C" const char* lnerf_last_error(void) { return g_last_error.c_str(); }

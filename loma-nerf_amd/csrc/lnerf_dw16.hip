@@ -38,8 +38,6 @@ typedef _Float16 hf4 __attribute__((ext_vector_type(4)));
 constexpr int kThreads = 512;
 constexpr int kRows = 512;                  // A rows [0, 256) and G rows [256, 512) of the image
 constexpr int kPlaneBytes = kRows * 32;     // one plane of a half-block: [row][16 samples] 16-bit
-constexpr int kImageBytes = 3 * kPlaneBytes;   // the largest image (PL = 3)
-constexpr int kLdsBytes = 2 * kImageBytes;  // double-buffered (96 KiB)
 // PL planes per operand: 3 = bf16x6, 2 = fp16x3 (x 2^e = hi + lo, the slab's layer-wide shift)
 template <int PL>
 constexpr int image_bytes() { return PL * kPlaneBytes; }

@@ -162,6 +162,7 @@ struct FusedPlan {
     int* wexp16;                         // x6 = 2: per-layer max|W| bits (fp16 weight plane shifts)
     int* smax16;                         // x6 = 2: per-slab max bits ([l] input of layer l, [L+l] G_l)
     float* smax_part;                    // x6 = 2: k1's per-wave slab maxima [2L][num_wg * 8]
+    int kact;                            // 1: k1 is kact_fwd_bwd_kernel (lnerf_kact.hip)
 };
 
 bool fused_supported(const lnerf_mlp& mlp, int rays, int S, int input_mode, const char** why);
@@ -177,6 +178,10 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
 void fused_render(const FusedPlan& p, const float* ws, const float* bs, const lnerf_batch& b,
                   const lnerf_outputs& out, hipStream_t s);
 void dw16_launch(const FusedPlan& p, hipStream_t s);
+// kact kernel entry points (lnerf_kact.hip): the fp16x3 k1 with the activations in LDS
+bool kact_supported(const FusedPlan& p);
+void kact_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lnerf_outputs& out,
+                 bool want_grad, hipStream_t s);
 // k16 kernel entry points (lnerf_k16.hip)
 bool k16_supported(const FusedPlan& p);
 void k16_pack(const FusedPlan& p, const float* ws, const float* bs, hipStream_t s);

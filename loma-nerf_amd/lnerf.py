@@ -46,6 +46,7 @@ PATH_GENERIC = 1
 PATH_FUSED = 2
 PATH_K16 = 4
 PATH_DW16 = 8
+PATH_KACT = 16
 
 
 class LnerfMLP(ctypes.Structure):
@@ -307,7 +308,8 @@ class Engine:
         if v < 0:
             raise RuntimeError(f"lnerf_ctx_last_path: {last_error()}")
         return dict(generic=bool(v & PATH_GENERIC), fused=bool(v & PATH_FUSED),
-                    k16=bool(v & PATH_K16), dw16=bool(v & PATH_DW16), planes=(v >> 8) & 3)
+                    k16=bool(v & PATH_K16), kact=bool(v & PATH_KACT), dw16=bool(v & PATH_DW16),
+                    planes=(v >> 8) & 3)
 
     def scale_by_device_scalar(self, buf, scale):
         rc = self.lib.lnerf_scale_by_device_scalar(ctypes.c_void_p(buf.data_ptr()), buf.numel(),

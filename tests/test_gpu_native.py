@@ -127,7 +127,9 @@ def test_fused_deep_mlp(engine, prec):
     path = engine.last_path()
     want_planes = {0: 2, 64: 0, 128: 1, 512: 3}[prec]
     assert path["fused"] and path["planes"] == want_planes, path
-    assert path["k16"] == (prec != 64), path
+    # fp16x3 (the default) on kact, bf16 / bf16x6 on k16
+    assert path["kact"] == (prec == 0), path
+    assert path["k16"] == (prec in (128, 512)), path
     assert path["dw16"] == (prec in (0, 512)), path
     want = oracle_ref(w)
     if prec == 128:
@@ -138,17 +140,23 @@ def test_fused_deep_mlp(engine, prec):
         compare(got, want)
 
 
-def test_default_path_is_k16_dw16(engine):
-    """The bench configuration (cfg3 MLP) runs k16 + dw16 with the fp16x3 split by default, and
-    the one-wave kernel with the bf16x6 split when k16 is switched off."""
+def test_default_path_is_kact_dw16(engine):
+    """The bench configuration (cfg3 MLP) runs kact + dw16 with the fp16x3 split by default, k16
+    when kact is switched off, and the one-wave kernel with the bf16x6 split without k16."""
     import os
     w = nerf_np.make_workload("cfg3", rays=8)
     run_native(engine, w, per_ray=False)
-    assert engine.last_path() == dict(generic=False, fused=True, k16=True, dw16=True, planes=2)
+    assert engine.last_path() == dict(generic=False, fused=True, k16=False, kact=True, dw16=True, planes=2)
+    os.environ["LNERF_KACT"] = "0"
+    try:
+        run_native(engine, w, per_ray=False)
+        assert engine.last_path() == dict(generic=False, fused=True, k16=True, kact=False, dw16=True, planes=2)
+    finally:
+        del os.environ["LNERF_KACT"]
     os.environ["LNERF_K16"] = "0"
     try:
         run_native(engine, w, per_ray=False)
-        assert engine.last_path() == dict(generic=False, fused=True, k16=False, dw16=True, planes=3)
+        assert engine.last_path() == dict(generic=False, fused=True, k16=False, kact=False, dw16=True, planes=3)
     finally:
         del os.environ["LNERF_K16"]
 

@@ -2,7 +2,7 @@
 # summed per kernel name: utilisation, instruction mix, LDS activity.
 set -u
 R="$GRAFT_REPO_ROOT"
-mkdir -p "$R/gpurun_out/pmc"
+mkdir -p "$R/gpurun_out/pmc"; rm -rf "$R/gpurun_out/pmc/p"*
 cd /tmp && export TMPDIR=/tmp
 LIBARG=""
 P1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS"
@@ -20,7 +20,7 @@ cnt = collections.defaultdict(lambda: collections.defaultdict(int))
 for f in glob.glob(sys.argv[1] + "/gpurun_out/pmc/p*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].replace("lnerf::(anonymous namespace)::", "").split("(")[0].replace("void ", "")
-        if "k16_fwd" in k or "dw16" in k:
+        if "k16_fwd" in k or "kact" in k:
             agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
             cnt[k][r["Counter_Name"]] += 1
 for k, d in agg.items():

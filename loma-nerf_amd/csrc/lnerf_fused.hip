@@ -1716,9 +1716,10 @@ void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws
     // LNERF_K16=0 selects the one-wave-per-SIMD kernel (fused_fwd_bwd_kernel) for A/B runs
     // (k16_wanted implies k16_supported: x6 is 1 or 3 and the head fits one tile)
     p.k16 = k16_wanted && k16_supported(p) ? 1 : 0;
-    // fp16x3 on k16's packing: kact (activations in LDS) unless LNERF_KACT=0
+    // fp16x3: kact (activations in LDS, 32x32 MFMA) with LNERF_KACT=1; k16 by default (kact is
+    // 1-3 % slower on cfg3)
     const char* ek = getenv("LNERF_KACT");
-    p.kact = p.k16 && !(ek && ek[0] == '0') && kact_supported(p) ? 1 : 0;
+    p.kact = p.k16 && (ek && ek[0] == '1') && kact_supported(p) ? 1 : 0;
     // dW: dw16_kernel for the bf16x6 split (LNERF_DW16=0: dw_all_kernel); one partial per split
     const char* e2 = getenv("LNERF_DW16");
     p.dw16 = (e2 && e2[0] == '0') ? 0 : (p.x6 == 3 || p.x6 == 2 ? 1 : 0);
@@ -1855,7 +1856,8 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
         if (ev) (void)hipEventRecord(ev[i], s);
     };
     mark(0);
-    if (p.k16) k16_pack(p, ws, bs, s);
+    if (p.kact) kact_pack(p, ws, bs, s);
+    else if (p.k16) k16_pack(p, ws, bs, s);
     else launch_pack(p, ws, bs, s);
     mark(1);
     if (p.kact) {
@@ -1931,7 +1933,7 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
 void fused_render(const FusedPlan& p, const float* ws, const float* bs, const lnerf_batch& b,
                   const lnerf_outputs& out, hipStream_t s) {
     if (p.kact) {
-        k16_pack(p, ws, bs, s);
+        kact_pack(p, ws, bs, s);
         kact_launch(p, b, 1.0f, out, false, s);
     } else if (p.k16) {
         k16_pack(p, ws, bs, s);

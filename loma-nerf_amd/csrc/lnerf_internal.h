@@ -180,6 +180,7 @@ void fused_render(const FusedPlan& p, const float* ws, const float* bs, const ln
 void dw16_launch(const FusedPlan& p, hipStream_t s);
 // kact kernel entry points (lnerf_kact.hip): the fp16x3 k1 with the activations in LDS
 bool kact_supported(const FusedPlan& p);
+void kact_pack(const FusedPlan& p, const float* ws, const float* bs, hipStream_t s);
 void kact_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lnerf_outputs& out,
                  bool want_grad, hipStream_t s);
 // k16 kernel entry points (lnerf_k16.hip)

@@ -127,9 +127,10 @@ def test_fused_deep_mlp(engine, prec):
     path = engine.last_path()
     want_planes = {0: 2, 64: 0, 128: 1, 512: 3}[prec]
     assert path["fused"] and path["planes"] == want_planes, path
-    # fp16x3 (the default) on kact, bf16 / bf16x6 on k16
-    assert path["kact"] == (prec == 0), path
-    assert path["k16"] == (prec in (128, 512)), path
+    # every bf16 / fp16 precision on k16 by default; fp16x3 on kact with LNERF_KACT=1
+    import os
+    want_kact = prec == 0 and os.environ.get("LNERF_KACT") == "1"
+    assert path["kact"] == want_kact and path["k16"] == (prec != 64 and not want_kact), path
     assert path["dw16"] == (prec in (0, 512)), path
     want = oracle_ref(w)
     if prec == 128:
@@ -140,17 +141,17 @@ def test_fused_deep_mlp(engine, prec):
         compare(got, want)
 
 
-def test_default_path_is_kact_dw16(engine):
-    """The bench configuration (cfg3 MLP) runs kact + dw16 with the fp16x3 split by default, k16
-    when kact is switched off, and the one-wave kernel with the bf16x6 split without k16."""
+def test_default_path_is_k16_dw16(engine):
+    """The bench configuration (cfg3 MLP) runs k16 + dw16 with the fp16x3 split by default, kact
+    with LNERF_KACT=1, and the one-wave kernel with the bf16x6 split without k16."""
     import os
     w = nerf_np.make_workload("cfg3", rays=8)
     run_native(engine, w, per_ray=False)
-    assert engine.last_path() == dict(generic=False, fused=True, k16=False, kact=True, dw16=True, planes=2)
-    os.environ["LNERF_KACT"] = "0"
+    assert engine.last_path() == dict(generic=False, fused=True, k16=True, kact=False, dw16=True, planes=2)
+    os.environ["LNERF_KACT"] = "1"
     try:
         run_native(engine, w, per_ray=False)
-        assert engine.last_path() == dict(generic=False, fused=True, k16=True, kact=False, dw16=True, planes=2)
+        assert engine.last_path() == dict(generic=False, fused=True, k16=False, kact=True, dw16=True, planes=2)
     finally:
         del os.environ["LNERF_KACT"]
     os.environ["LNERF_K16"] = "0"
@@ -439,3 +440,51 @@ def test_render_image_bf16_close_to_fp32_accurate(engine):
     want = oracle.standard_forward_backward(Xs, wp, bp, shapes, dists[sub],
                                             np.zeros((len(sub), 3), np.float32), 128, seed=1.0)
     assert_close("acc", a[sub], want["acc"], **TOL)
+
+
+# ---- kact (LNERF_KACT=1: activations in LDS, fp16x3 on 32x32x16 MFMAs) through the same checks --
+
+KACT_CASES = ["cfg2_points", "cfg2_encoded", "cfg3", "nonuniform", "deep", "ragged", "dx", "render", "rays",
+              "golden:chunk_4x30.npz", "golden:deep8_w64_2x64.npz", "golden:trained_weights_8x16.npz"]
+
+
+@pytest.mark.parametrize("case", KACT_CASES)
+def test_kact_matches_oracle(engine, case, monkeypatch):
+    """The opt-in kact kernel against the oracle / fixtures on the k16 tests' workloads, and the
+    path report proving it ran."""
+    monkeypatch.setenv("LNERF_KACT", "1")
+    if case == "cfg2_points":
+        test_fused_cfg2_matches_oracle(engine, True, 0)
+    elif case == "cfg2_encoded":
+        test_fused_cfg2_matches_oracle(engine, False, 0)
+    elif case == "cfg3":
+        test_fused_cfg3_subset_matches_oracle(engine, 0)
+    elif case == "nonuniform":
+        test_fused_nonuniform_widths(engine, 0)
+    elif case == "deep":
+        test_fused_deep_mlp(engine, 0)
+    elif case == "ragged":
+        test_fused_ragged_rays_and_samples(engine)
+    elif case == "dx":
+        test_fused_dx_encoded(engine)
+    elif case == "render":
+        test_render_forward_only_matches_train_forward(engine)
+    elif case == "rays":
+        test_rays_mode_matches_oracle(engine, False)
+    else:
+        test_fused_matches_golden_fixture(engine, case.split(":", 1)[1], 0)
+    assert engine.last_path()["kact"], engine.last_path()
+
+
+def test_kact_full_size_determinism_and_fused_vs_generic(engine, full_noties, monkeypatch):
+    """kact at the bench size: bitwise run-to-run determinism and parity with the loma-order
+    generic path on the tie-free rays."""
+    import lnerf
+    monkeypatch.setenv("LNERF_KACT", "1")
+    a = run_native(engine, full_noties, seed=1.0)
+    assert engine.last_path()["kact"]
+    a2 = run_native(engine, full_noties, seed=1.0)
+    for k in ("dW", "dB", "d_dists", "d_target"):
+        assert np.array_equal(a[k], a2[k]), k
+    b = run_native(engine, full_noties, seed=1.0, flags=lnerf.GENERIC)
+    compare(a, b)

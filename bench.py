@@ -6,8 +6,9 @@ Workload (BASELINE.json configs[2]): synthetic Lego-sty
 random-init weights (mlp_utils.py:166-204, seed 215). A step = sampling the rays (linspace depths,
 points, dists; train_nerf.py:289-306) + positional encoding + MLP forward + compositing +
 sum-of-squares loss + the reverse pass over every MLP weight (the work of one
-nerf_evaluate_and_march + grad_nerf_evaluate_and_march pair on the batch), on rays already
-resident in HBM (--input points: host-sampled points instead). With N > 1 GPUs (one process per GPU, torchrun) every rank runs its own 4096-ray
+nerf_evaluate_and_march + grad_nerf_evaluate_and_march pair on the batch) + the reference's Adam
+update of every weight and bias on the device (train_nerf.py:133-161; --no-optimizer drops it), on
+rays already resident in HBM (--input points: host-sampled points instead). With N > 1 GPUs (one process per GPU, torchrun) every rank runs its own 4096-ray
 batch (weak scaling) and the packed [dW, db, loss] buffer is all-reduced (SUM) over RCCL, then
 scaled by the global loss (the reference seeds its gradient with the loss, train_nerf.py:477).
 
@@ -57,6 +58,10 @@ def parse():
                     help="fused path with exact f32 MFMA products instead of the bf16x6 split")
     ap.add_argument("--x6-train", action="store_true",
                     help="fused path with the bf16x6 split instead of the default fp16x3 split")
+    ap.add_argument("--no-optimizer", action="store_true",
+                    help="fwd+bwd only: skip the on-device Adam update (train_nerf.py:133-161) "
+                         "that every timed step otherwise applies after the gradient exchange")
+    ap.add_argument("--lr", type=float, default=5e-4, help="Adam learning rate (train_nerf.py)")
     return ap.parse_args()
 
 
@@ -120,8 +125,14 @@ def bench_render(args, world, rank, local, dist):
     eng = lnerf.Engine(local)
     shapes, wp, bp = scene.init_mlp(3 + 6 * F, 4, L, H)
     mlp = lnerf.make_mlp(shapes, wp.shape[1], wp.shape[2])
-    ws = torch.from_numpy(wp).to(dev)
-    bs = torch.from_numpy(bp).to(dev)
+    # weights and biases packed like the gradient buffer [dW | db], so that one Adam launch
+    # updates both (padding entries have zero gradients and never move)
+    params = torch.cat([torch.from_numpy(wp).reshape(-1), torch.from_numpy(bp).reshape(-1)]).to(dev)
+    ws = params[:wp.size].view(wp.shape)
+    bs = params[wp.size:].view(bp.shape)
+    adam_m = torch.zeros_like(params)
+    adam_v = torch.zeros_like(params)
+    adam_t = [0]
     focal = 0.5 / np.tan(0.5 * scene.CAMERA_ANGLE_X)
     K = np.array([[focal, 0, 0.5], [0, focal, 0.5], [0, 0, 1]])
     rays_all = eng.get_rays(side, K, scene.look_at_pose())
@@ -212,8 +223,14 @@ def main():
     N, S = b["N"], b["S"]
     eng = lnerf.Engine(local)
     mlp = lnerf.make_mlp(shapes, wp.shape[1], wp.shape[2])
-    ws = torch.from_numpy(wp).to(dev)
-    bs = torch.from_numpy(bp).to(dev)
+    # weights and biases packed like the gradient buffer [dW | db], so that one Adam launch
+    # updates both (padding entries have zero gradients and never move)
+    params = torch.cat([torch.from_numpy(wp).reshape(-1), torch.from_numpy(bp).reshape(-1)]).to(dev)
+    ws = params[:wp.size].view(wp.shape)
+    bs = params[wp.size:].view(bp.shape)
+    adam_m = torch.zeros_like(params)
+    adam_v = torch.zeros_like(params)
+    adam_t = [0]
     if args.input == "rays":
         x = torch.from_numpy(b["rays"]).to(dev)
         dists = None
@@ -242,6 +259,11 @@ def main():
                            seed=1.0, flags=f, grads=grads, acc_color=acc)
             # [dW, db, loss] SUM over ranks (RCCL), then the loss seed (loma-nerf_amd/dp.py)
             dp.allreduce_loss_seeded(gbuf, dist, eng.scale_by_device_scalar)
+        if not args.no_optimizer:
+            # the reference's Adam step on the device (replicated on every rank after the
+            # all-reduce, so weights stay identical)
+            adam_t[0] += 1
+            eng.adam_update(params, gbuf[:-1], adam_m, adam_v, adam_t[0], args.lr)
 
     for _ in range(args.warmup):
         step()
@@ -291,6 +313,8 @@ def main():
                                    f"MLP {shapes[0][0]}->{b['H']}x{b['L'] - 1}->4, fp32",
                        "rays_per_gpu": N, "samples": S, "layers": b["L"], "width": b["H"],
                        "parallelism": f"dp{world}", "path": "generic" if args.generic else "fused",
+                       "optimizer": (None if args.no_optimizer else
+                                     f"adam lr {args.lr} on device (train_nerf.py:133-161), in the step"),
                        "input": ("rays: sampling, dists and positional encoding on the GPU"
                                  if args.input == "rays" else "points: sampled on the host")},
             "step_tflops": step_flops / (ms / 1e3) / 1e12,

@@ -403,20 +403,52 @@ __global__ void __launch_bounds__(kThreads, 1) dw16_kernel(Dw16Args a) {
     }
 }
 
-// PL = 2: slab blockIdx.x's layer-wide max from k1's per-wave maxima (n per slab), as the bits of
-// a non-negative float in smax[slab]
-__global__ void slab_max_reduce_kernel(const float* __restrict__ part, int n, int* __restrict__ smax) {
-    const float* q = part + (size_t)blockIdx.x * n;
-    float m = 0.0f;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) m = fmaxf(m, q[i]);
-    __shared__ float red[256];
-    red[threadIdx.x] = m;
+// The reductions between k1 and dw16 in one launch (1024 threads per block):
+//  * blocks [0, nslab): PL = 2, slab b's layer-wide max from k1's per-wave maxima (n per slab), as
+//    the bits of a non-negative float in smax[b] (the exponent shifts dw16 splits with);
+//  * block nslab: the batch loss, the same deterministic 256-lane tree as loss_reduce_kernel
+//    (lnerf_fused.hip), into *total (the loss seed) and *out_loss.
+__global__ void __launch_bounds__(1024) k1_reduce_kernel(const float* __restrict__ part, int n,
+                                                         int* __restrict__ smax, int nslab,
+                                                         const float* __restrict__ loss_part, int nwg,
+                                                         float* total, float* out_loss) {
+    __shared__ float red[1024];
+    const int t = threadIdx.x;
+    if ((int)blockIdx.x < nslab) {
+        const float* q = part + (size_t)blockIdx.x * n;
+        float m = 0.0f;
+        if ((n & 3) == 0) {
+            const float4* q4 = reinterpret_cast<const float4*>(q);
+            for (int i = t; i < (n >> 2); i += 1024) {
+                const float4 v = q4[i];
+                m = fmaxf(fmaxf(m, fmaxf(v.x, v.y)), fmaxf(v.z, v.w));
+            }
+        } else {
+            for (int i = t; i < n; i += 1024) m = fmaxf(m, q[i]);
+        }
+        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+        if ((t & 63) == 0) red[t >> 6] = m;
+        __syncthreads();
+        if (t == 0) {
+            float r = red[0];
+            for (int w = 1; w < 16; ++w) r = fmaxf(r, red[w]);
+            smax[blockIdx.x] = __float_as_int(r);
+        }
+        return;
+    }
+    float s = 0.0f;
+    if (t < 256)
+        for (int i = t; i < nwg; i += 256) s += loss_part[i];
+    red[t] = s;
     __syncthreads();
     for (int w = 128; w > 0; w >>= 1) {
-        if ((int)threadIdx.x < w) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + w]);
+        if (t < w) red[t] = red[t] + red[t + w];
         __syncthreads();
     }
-    if (threadIdx.x == 0) smax[blockIdx.x] = __float_as_int(red[0]);
+    if (t == 0) {
+        *total = red[0];
+        if (out_loss) *out_loss = red[0];
+    }
 }
 
 }  // namespace
@@ -443,11 +475,15 @@ void dw16_launch(const FusedPlan& p, hipStream_t s) {
     a.db_part = p.db_part;
     a.smax = p.smax16;
     a.L = p.L;
-    if (p.x6 == 2) {
-        slab_max_reduce_kernel<<<2 * p.L, 256, 0, s>>>(p.smax_part, p.num_wg * 8, p.smax16);
-        dw16_kernel<2><<<p.dw_grid, kThreads, 0, s>>>(a);
-    }
+    // PL = 2 needs the slab maxima of k1_reduce_launch (launched right after k1)
+    if (p.x6 == 2) dw16_kernel<2><<<p.dw_grid, kThreads, 0, s>>>(a);
     else dw16_kernel<3><<<p.dw_grid, kThreads, 0, s>>>(a);
+}
+
+void k1_reduce_launch(const FusedPlan& p, float* out_loss, hipStream_t s) {
+    const int nslab = (p.dw16 && p.x6 == 2) ? 2 * p.L : 0;
+    k1_reduce_kernel<<<nslab + 1, 1024, 0, s>>>(p.smax_part, p.num_wg * 8, p.smax16, nslab, p.loss_part,
+                                                p.num_wg, p.loss_total, out_loss);
 }
 
 }  // namespace lnerf

@@ -1614,6 +1614,7 @@ size_t fused_workspace_bytes(const lnerf_mlp& m, int rays, int S, bool train) {
                align_up((size_t)y.num_wg, 64) + align_up(y.dwp_total, 64) + align_up(y.dbp_total, 64) +
                64 + align_up((y.w16_total + 1) / 2, 64) + align_up(y.b16_total, 64) +
                align_up(y.mask_total * 2, 64) + 64 +   // + the fp16x3 weight/slab maxima
+               align_up((size_t)kMaxLayers * kWmaxParts, 64) +   // + per-block max|W| partials
                (train ? align_up((size_t)2 * m.num_layers * y.num_wg * 8, 64) : 0);
     return f * sizeof(float);
 }
@@ -1700,6 +1701,8 @@ void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws
     p.wexp16 = (int*)(base + off);
     p.smax16 = p.wexp16 + kMaxLayers;
     off += 64;
+    p.wmax_part = (int*)(base + off);
+    off += align_up((size_t)kMaxLayers * kWmaxParts, 64);
     p.smax_part = base + off;
     if (train) off += align_up((size_t)2 * p.L * y.num_wg * 8, 64);
 
@@ -1872,7 +1875,7 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
     prof_report(p, s);
 #endif
     mark(2);
-    loss_reduce_kernel<<<1, 256, 0, s>>>(p.loss_part, p.num_wg, p.loss_total, out.loss);
+    k1_reduce_launch(p, out.loss, s);
     mark(3);
     DwArgs da{};
     da.L = p.L;

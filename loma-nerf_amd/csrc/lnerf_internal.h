@@ -10,6 +10,7 @@
 namespace lnerf {
 
 constexpr int kMaxLayers = LNERF_MAX_LAYERS;
+constexpr int kWmaxParts = 32;   // blocks per layer of the max|W| pass before the fp16x3 packing
 
 // ---- ray sampling (train_nerf.py:289-306), float64 as numpy computes it -----------------------
 // t_j = np.linspace(near, far, S)[j]: j * ((far - near) / (S - 1)) + near, the last one = far.
@@ -160,6 +161,7 @@ struct FusedPlan {
     unsigned long long* mask_g;          // [num_wg][L-1][8 waves][64 lanes] ReLU mask bits
     int dw16;                            // 1: dW by dw16_kernel (lnerf_dw16.hip), one partial per split
     int* wexp16;                         // x6 = 2: per-layer max|W| bits (fp16 weight plane shifts)
+    int* wmax_part;                      // x6 = 2: max|W| bits per layer and wmax block [L][kWmaxParts]
     int* smax16;                         // x6 = 2: per-slab max bits ([l] input of layer l, [L+l] G_l)
     float* smax_part;                    // x6 = 2: k1's per-wave slab maxima [2L][num_wg * 8]
     int kact;                            // 1: k1 is kact_fwd_bwd_kernel (lnerf_kact.hip)
@@ -178,6 +180,9 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
 void fused_render(const FusedPlan& p, const float* ws, const float* bs, const lnerf_batch& b,
                   const lnerf_outputs& out, hipStream_t s);
 void dw16_launch(const FusedPlan& p, hipStream_t s);
+// after a training k1: the batch loss (loss_total, out_loss) and, for dw16 with x6 = 2, the
+// layer-wide slab maxima, in one launch (lnerf_dw16.hip)
+void k1_reduce_launch(const FusedPlan& p, float* out_loss, hipStream_t s);
 // kact kernel entry points (lnerf_kact.hip): the fp16x3 k1 with the activations in LDS
 bool kact_supported(const FusedPlan& p);
 void kact_pack(const FusedPlan& p, const float* ws, const float* bs, hipStream_t s);

@@ -744,32 +744,45 @@ struct Pack16Args {
     unsigned short* w16;
     size_t wf_off[kMaxLayers], wb_off[kMaxLayers];
     float* b16;
-    int* wexp;   // planes = 2: per-layer max|W| bits (wmax16_kernel)
+    int* wexp;   // planes = 2: per-layer max|W| bits (pack16_kernel, from wmax16_kernel partials)
+    int* wpart;  // [L][kWmaxParts] partial max|W| bits
 };
 
-// planes = 2: max|W_l| per layer as the bits of a non-negative float (integer order = float
-// order), grid (64, L): each block folds its rows into one atomicMax on a.wexp[l] (zeroed first).
-__global__ void wmax16_kernel(Pack16Args a) {
+// planes = 2: max|W_l| as the bits of a non-negative float (integer order = float order), one
+// partial per block, grid (kWmaxParts, L): plain stores, no zeroing launch and no atomics; the
+// packing kernel folds the layer's kWmaxParts partials itself.
+__global__ void __launch_bounds__(256) wmax16_kernel(Pack16Args a) {
     const int l = blockIdx.y;
     const float* W = a.W + (size_t)l * a.w_k * a.w_n;
     const int K = a.k[l], N = a.n[l];
     float m = 0.0f;
     for (int k = blockIdx.x; k < K; k += gridDim.x)
         for (int j = threadIdx.x; j < N; j += blockDim.x) m = fmaxf(m, fabsf(W[(size_t)k * a.w_n + j]));
-    __shared__ float red[256];
-    red[threadIdx.x] = m;
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    __shared__ float red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
     __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if ((int)threadIdx.x < w) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + w]);
-        __syncthreads();
-    }
-    if (threadIdx.x == 0 && red[0] > 0.0f) atomicMax(&a.wexp[l], __float_as_int(red[0]));
+    if (threadIdx.x == 0)   // fmaxf drops NaNs: the max is finite, +inf or 0
+        a.wpart[l * kWmaxParts + blockIdx.x] =
+            __float_as_int(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+}
+
+// the layer's max|W| bits from its kWmaxParts partials (uniform per block); block (0, l) also
+// publishes them in wexp[l] for k1
+__device__ __forceinline__ int layer_wmax(Pack16Args& a, int l) {
+    int mb = 0;
+    for (int i = 0; i < kWmaxParts; ++i) mb = max(mb, a.wpart[l * kWmaxParts + i]);
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.wexp[l] = mb;
+    return mb;
 }
 
 
-__global__ void pack16_kernel(Pack16Args a, int l) {
+// every layer in one launch: grid (blocks of the largest layer, L)
+__global__ void pack16_kernel(Pack16Args a) {
+    const int l = blockIdx.y;
     const float* W = a.W + (size_t)l * a.w_k * a.w_n;
     const int K = a.k[l], N = a.n[l];
+    const int wsh = a.planes == 2 ? wshift_of(layer_wmax(a, l)) : 0;
     const size_t nf = (size_t)a.ks_f[l] * a.to_f[l] * 512, nb = (size_t)a.ks_b[l] * a.to_b[l] * 512;
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < nf + nb + 256;
          e += (size_t)gridDim.x * blockDim.x) {
@@ -792,7 +805,7 @@ __global__ void pack16_kernel(Pack16Args a, int l) {
                               ((size_t)(s * to + o) * a.planes) * 512 + ln * 8 + j;
         if (a.planes == 2) {
             _Float16 h, lo;
-            split_h(__builtin_ldexpf(w, wshift_of(a.wexp[l])), h, lo);
+            split_h(__builtin_ldexpf(w, wsh), h, lo);
             dst[0] = __builtin_bit_cast(unsigned short, h);
             dst[512] = __builtin_bit_cast(unsigned short, lo);
             continue;
@@ -836,14 +849,14 @@ void k16_pack(const FusedPlan& p, const float* ws, const float* bs, hipStream_t 
     a.w16 = p.w16;
     a.b16 = p.b16;
     a.wexp = p.wexp16;
-    if (a.planes == 2) {
-        (void)hipMemsetAsync(p.wexp16, 0, sizeof(int) * p.L, s);
-        wmax16_kernel<<<dim3(64, p.L), 256, 0, s>>>(a);
-    }
+    a.wpart = p.wmax_part;
+    if (a.planes == 2) wmax16_kernel<<<dim3(kWmaxParts, p.L), 256, 0, s>>>(a);
+    size_t nmax = 0;
     for (int l = 0; l < p.L; ++l) {
         const size_t nel = ((size_t)a.ks_f[l] * a.to_f[l] + (size_t)a.ks_b[l] * a.to_b[l]) * 512 + 256;
-        pack16_kernel<<<(unsigned)((nel + 255) / 256), 256, 0, s>>>(a, l);
+        nmax = nel > nmax ? nel : nmax;
     }
+    pack16_kernel<<<dim3((unsigned)((nmax + 255) / 256), p.L), 256, 0, s>>>(a);
 }
 
 void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lnerf_outputs& out,

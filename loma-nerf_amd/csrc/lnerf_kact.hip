@@ -841,31 +841,45 @@ struct PackArgs {
     unsigned short* w;
     float* b16;
     int* wexp;
+    int* wpart;  // [L][kWmaxParts] partial max|W| bits
 };
 
-__global__ void kact_wmax_kernel(PackArgs a) {
+// planes = 2: max|W_l| as the bits of a non-negative float (integer order = float order), one
+// partial per block, grid (kWmaxParts, L): plain stores, no zeroing launch and no atomics; the
+// packing kernel folds the layer's kWmaxParts partials itself.
+__global__ void __launch_bounds__(256) kact_wmax_kernel(PackArgs a) {
     const int l = blockIdx.y;
     const float* W = a.W + (size_t)l * a.w_k * a.w_n;
     const int K = a.k[l], N = a.n[l];
     float m = 0.0f;
     for (int k = blockIdx.x; k < K; k += gridDim.x)
         for (int j = threadIdx.x; j < N; j += blockDim.x) m = fmaxf(m, fabsf(W[(size_t)k * a.w_n + j]));
-    __shared__ float red[256];
-    red[threadIdx.x] = m;
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    __shared__ float red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
     __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if ((int)threadIdx.x < w) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + w]);
-        __syncthreads();
-    }
-    if (threadIdx.x == 0 && red[0] > 0.0f) atomicMax(&a.wexp[l], __float_as_int(red[0]));
+    if (threadIdx.x == 0)   // fmaxf drops NaNs: the max is finite, +inf or 0
+        a.wpart[l * kWmaxParts + blockIdx.x] =
+            __float_as_int(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+}
+
+// the layer's max|W| bits from its kWmaxParts partials (uniform per block); block (0, l) also
+// publishes them in wexp[l] for k1
+__device__ __forceinline__ int layer_wmax(PackArgs& a, int l) {
+    int mb = 0;
+    for (int i = 0; i < kWmaxParts; ++i) mb = max(mb, a.wpart[l * kWmaxParts + i]);
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.wexp[l] = mb;
+    return mb;
 }
 
 // fragment (u, t, plane) lane ln element e: row o = 32 t + (ln & 31), K index psi(u, 8 (ln >> 5) + e);
 // forward W[k = psi][o], backward W[o][psi]
-__global__ void kact_pack_kernel(PackArgs a, int l) {
+// every layer in one launch: grid (blocks of the largest layer, L)
+__global__ void kact_pack_kernel(PackArgs a) {
+    const int l = blockIdx.y;
     const float* W = a.W + (size_t)l * a.w_k * a.w_n;
     const int K = a.k[l], N = a.n[l];
-    const int ws = shift_of(__int_as_float(a.wexp[l]));
+    const int ws = shift_of(__int_as_float(layer_wmax(a, l)));
     const size_t nf = (size_t)a.ks_f[l] * a.to_f[l] * 512, nb = (size_t)a.ks_b[l] * a.to_b[l] * 512;
     for (size_t x0 = blockIdx.x * (size_t)blockDim.x + threadIdx.x; x0 < nf + nb + 256;
          x0 += (size_t)gridDim.x * blockDim.x) {
@@ -959,12 +973,14 @@ void kact_pack(const FusedPlan& p, const float* ws, const float* bs, hipStream_t
     a.w = p.w16;
     a.b16 = p.b16;
     a.wexp = p.wexp16;
-    (void)hipMemsetAsync(p.wexp16, 0, sizeof(int) * p.L, s);
-    kact_wmax_kernel<<<dim3(64, p.L), 256, 0, s>>>(a);
+    a.wpart = p.wmax_part;
+    kact_wmax_kernel<<<dim3(kWmaxParts, p.L), 256, 0, s>>>(a);
+    size_t nmax = 0;
     for (int l = 0; l < p.L; ++l) {
         const size_t nel = ((size_t)y.ks_f[l] * y.to_f[l] + (size_t)y.ks_b[l] * y.to_b[l]) * 512 + 256;
-        kact_pack_kernel<<<(unsigned)((nel + 255) / 256), 256, 0, s>>>(a, l);
+        nmax = nel > nmax ? nel : nmax;
     }
+    kact_pack_kernel<<<dim3((unsigned)((nmax + 255) / 256), p.L), 256, 0, s>>>(a);
 }
 
 void kact_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lnerf_outputs& out,

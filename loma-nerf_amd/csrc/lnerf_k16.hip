@@ -483,7 +483,7 @@ __device__ __forceinline__ int shift_of(float m) {
 }
 
 // PL = 2, training: the wave's max of a slab, one plain store per wave and slab into
-// smax_part[slab][global wave] (slab_max_reduce folds them into dw16's layer-wide exponent
+// smax_part[slab][global wave] (k1_reduce_kernel folds them into dw16's layer-wide exponent
 // shifts; an atomic per wave on 2L shared words measured 2.2x slower for the whole kernel).
 // Issued before the pass's first DMA, so it is older than every piece a dma_barrier waits for.
 __device__ __forceinline__ void slab_max(float* part, int slab, float m) {

@@ -348,6 +348,14 @@ def main():
             out["kernels_ms"] = kt
             out["dw_kernel_tflops"] = dw_flops / (kt["dw"] / 1e3) / 1e12
             out["dw_kernel_frac"] = out["dw_kernel_tflops"] / peak
+            # k2 streams the slabs k1 wrote: algorithmic bytes = every slab value read once
+            # (X, A_l for l < L-1, G_l for every l; 32-feature tiles, fp32)
+            slab_b = 4 * 32 * (-(-shapes[0][0] // 32) + sum(-(-n // 32) for _, n in shapes[:-1])
+                               + sum(-(-n // 32) for _, n in shapes))
+            out["dw_kernel_hbm"] = {"bytes_per_sample": slab_b, "bytes_per_launch": slab_b * N * S,
+                                    "achieved_gbs": slab_b * N * S / (kt["dw"] / 1e3) / 1e9,
+                                    "peak_gbs": PEAK_HBM_GBS,
+                                    "frac": slab_b * N * S / (kt["dw"] / 1e3) / 1e9 / PEAK_HBM_GBS}
         if world == 1 and not args.no_cpu_baseline:
             c1, cn = cpu_baseline(args, args.config)
             out["cpu_baseline"] = c1

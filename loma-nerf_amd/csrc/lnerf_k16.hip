@@ -1,5 +1,6 @@
 // lnerf_k16.hip -- k1 on wave pairs: the fused PE + MLP + compositing + reverse chain with two
-// waves per SIMD (v_mfma_f32_16x16x32_bf16), the default fused kernel for the bf16 precisions.
+// waves per SIMD (v_mfma_f32_16x16x32_f16 / _bf16), the default fused kernel for every MFMA
+// precision but exact f32 (fp16x3 default, bf16x6, plain bf16 for inference).
 //
 // Same work and outputs as fused_fwd_bwd_kernel (lnerf_fused.hip; reference scripts/nerf.py:1-304
 // and its rev_diff, train_nerf.py:325/395), re-tiled so that a CU holds TWO waves per SIMD:
@@ -9,9 +10,10 @@
 //  * the activations stay in the transposed accumulator layout (lane = sample l & 15, registers
 //    = features 4(l >> 4) + i of each 16-feature tile), which is the next layer's B operand after
 //    a fixed permutation of the contraction order (phi below) baked into the weight packing;
-//  * the weights of one k-step (32 input features x every output tile, in the 3 bf16 planes of
-//    the bf16x6 split) stream through a 2-slot LDS ring by LDS-DMA (one chunk in flight while
-//    one is computed), one barrier per k-step;
+//  * the weights of one k-step (32 input features x every output tile, in the PL planes of the
+//    split: fp16 hi/lo for fp16x3, bf16 hi/mid/lo for bf16x6, one plane for plain bf16) stream
+//    through a 3-slot LDS ring by LDS-DMA (one chunk in flight while one is computed; the late
+//    waves of the staggered pairs still read the previous one), one barrier per k-step;
 //  * while one wave of a SIMD issues its LDS reads, operand splits, slab stores, DMA pieces or
 //    epilogue, its partner's MFMAs keep the matrix core busy -- the latency hiding that the
 //    one-wave-per-SIMD kernel had to hand-schedule.

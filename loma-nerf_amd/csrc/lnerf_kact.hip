@@ -1,5 +1,6 @@
 // lnerf_kact.hip -- k1 with the activations resident in LDS: the fused PE + MLP + compositing +
-// reverse chain for the fp16x3 split, the default fused kernel wherever it applies.
+// reverse chain for the fp16x3 split, opt-in with LNERF_KACT=1 (k16 stays the default: measured
+// 1.49-1.54 vs 1.47-1.50 ms at cfg3; DESIGN.md §3 has where kact's time goes).
 //
 // Same work and outputs as k16 (lnerf_k16.hip; reference scripts/nerf.py:1-304 and its rev_diff,
 // train_nerf.py:325/395), organised around v_mfma_f32_32x32x16_f16 in the transposed form

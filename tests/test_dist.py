@@ -2,7 +2,9 @@
 loma-nerf_amd/dp.py: each rank computes unit-seeded gradients of its ray shard (here with the C
 oracle standing in for the device kernels), one SUM all-reduce of the packed [dW | db | loss]
 buffer, then scaling by the reduced loss must equal the loss-seeded gradient of the full batch
-(train_nerf.py:477 seeds the gradient with the loss; the loss is a sum over rays)."""
+(train_nerf.py:477 seeds the gradient with the loss; the loss is a sum over rays). Every rank then
+applies the reference's Adam step (train_nerf.py:133-161) to its own replica of the parameters,
+and the replicas must stay bit-identical (no broadcast in the protocol)."""
 import os
 import socket
 
@@ -19,6 +21,15 @@ def _free_port():
     p = s.getsockname()[1]
     s.close()
     return p
+
+
+def _adam1(p, g, lr=5e-4, b1=0.9, b2=0.999, eps=1e-8):
+    """First AdamOptimizer.update of train_nerf.py:143-161 (float32 arrays, t = 1)."""
+    t = 1
+    lr_t = lr * (np.sqrt(1 - b2 ** t) / (1 - b1 ** t))
+    m = (1 - b1) * g
+    v = (1 - b2) * (g ** 2)
+    return p - lr_t * (m / (1 - b1 ** t)) / (np.sqrt(v / (1 - b2 ** t)) + eps)
 
 
 def _worker(rank, world, port, out):
@@ -42,8 +53,8 @@ def _worker(rank, world, port, out):
     packed = torch.from_numpy(np.concatenate([r["dW"].ravel(), r["dB"].ravel(),
                                               [np.float32(r["loss"])]]).astype(np.float32))
     dp.allreduce_loss_seeded(packed, dist)
-    if rank == 0:
-        out.put(packed.numpy().copy())
+    params = np.concatenate([w.wp.ravel(), w.bp.ravel()]).astype(np.float32)
+    out.put((rank, packed.numpy().copy(), _adam1(params, packed.numpy()[:-1])))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -58,10 +69,14 @@ def test_two_rank_gloo_allreduce_matches_full_batch(oracle_lib):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    got = q.get(timeout=120)
+    res = dict((r, (g, pn)) for r, g, pn in (q.get(timeout=120), q.get(timeout=120)))
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
+    got = res[0][0]
+    # the all-reduced buffer and the replicated Adam step are bit-identical on both ranks
+    assert np.array_equal(res[0][0], res[1][0])
+    assert np.array_equal(res[0][1], res[1][1])
     w = nerf_np.make_workload("cfg2", rays=20, samples=8)
     shapes = [x.shape for x in w.ws]
     full = oracle.standard_forward_backward(w.X, w.wp, w.bp, shapes, w.dists, w.target, w.S,
@@ -72,6 +87,14 @@ def test_two_rank_gloo_allreduce_matches_full_batch(oracle_lib):
     assert_close("dW", got[:nW].reshape(full["dW"].shape), full["dW"], rtol=1e-4, atol_scale=1e-5)
     assert_close("dB", got[nW:nW + nB].reshape(full["dB"].shape), full["dB"], rtol=1e-4,
                  atol_scale=1e-5)
+    # the replicated update equals Adam on the full-batch gradient, except where a gradient is
+    # so small that fp32 summation order decides its sign (Adam's first step is +-lr there)
+    p0 = np.concatenate([w.wp.ravel(), w.bp.ravel()]).astype(np.float32)
+    gfull = np.concatenate([full["dW"].ravel(), full["dB"].ravel()]).astype(np.float32)
+    want = _adam1(p0, gfull)
+    big = np.abs(gfull) > 1e-3 * np.abs(gfull).max()
+    assert big.sum() > 0.5 * (gfull != 0).sum()
+    assert np.allclose(res[0][1][big], want[big], rtol=1e-6, atol=1e-6)
 
 
 def test_shard_rays_partitions():

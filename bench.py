@@ -83,6 +83,25 @@ def pmc_traffic(kernel, config):
     return None
 
 
+def sq_counters(kernel):
+    """MFMA-busy and LDS figures for `kernel` from the newest committed SQ counter summary
+    (profiles/<round>_sq.json, scripts/gpu_sq.sh + scripts/summarize_sq.py: separate rocprofv3
+    --pmc passes of this bench), or None. mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8
+    x 1024 SIMDs), rocprof's MfmaUtil."""
+    import glob
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", "r*_sq.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    for name, v in d["kernels"].items():
+        if name.startswith(kernel):
+            der = v["derived"]
+            return {"mfma_busy": der.get("mfma_busy"), "lds_busy": der.get("lds_busy"),
+                    "lds_bank_conflict": der.get("lds_conflict"), "clock_ghz": der.get("clock_ghz"),
+                    "source": os.path.relpath(files[-1], HERE)}
+    return None
+
+
 def cpu_baseline(args, cfg):
     """The C oracle (loma-order scalar fp32 restatement, -O2, no FMA) timed on this host on a
     bounded sample of the same workload. Test infrastructure, used only as the reported baseline."""
@@ -323,11 +342,10 @@ def main():
             fus_ms = kt["fused"]
             peak = (PEAK_FP32_TFLOPS if args.mfma_f32 else PEAK_X6_TFLOPS if args.x6_train
                     else PEAK_F16X3_TFLOPS)
-            # the fused kernel the engine ran: kact (LDS-resident activations, the fp16x3
-            # default), k16 (wave pairs) or the one-wave-per-SIMD kernel (exact f32 MFMA)
+            # the fused kernel the engine ran: k16 (wave pairs, the default) or the
+            # one-wave-per-SIMD kernel (exact f32 MFMA / LNERF_ONE_WAVE)
             lp = eng.last_path()
-            k1 = ("kact_fwd_bwd_kernel" if lp["kact"] else "k16_fwd_bwd_kernel" if lp["k16"]
-                  else "fused_fwd_bwd_kernel")
+            k1 = "k16_fwd_bwd_kernel" if lp["k16"] else "fused_fwd_bwd_kernel"
             out["roofline"] = {"bound": "mfma", "kernel": k1,
                                "achieved": fused_flops / (fus_ms / 1e3) / 1e12,
                                "peak": peak, "unit": "TFLOP/s",
@@ -345,6 +363,10 @@ def main():
                 out["roofline"]["traffic_unit"] = "bytes/launch"
                 out["roofline"]["traffic_source"] = tr["source"]
                 out["roofline"]["traffic_gbs"] = tr["bytes"] / (fus_ms / 1e3) / 1e9
+            sq = sq_counters(k1) if args.rays is None and not (args.mfma_f32 or args.x6_train) else None
+            if sq:
+                out["roofline"]["mfma_busy"] = sq["mfma_busy"]
+                out["roofline"]["counters"] = sq
             out["kernels_ms"] = kt
             out["dw_kernel_tflops"] = dw_flops / (kt["dw"] / 1e3) / 1e12
             out["dw_kernel_frac"] = out["dw_kernel_tflops"] / peak

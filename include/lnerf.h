@@ -135,13 +135,26 @@ enum {
     LNERF_MFMA_BF16 = 128,    /* fused path: plain bf16 operands, fp32 accumulate (one MFMA per
                                  product; reduced precision -- inference / config 5 render)   */
     LNERF_MFMA_F16X3 = 256,   /* fused path: the fp16x3 split, the default wherever the k16
-                                 kernel runs: x 2^e = hi + lo in fp16 with per-sample and
-                                 per-layer exponent shifts, three fp16 MFMAs per product
-                                 (dropped terms <= ~3 2^-22 |w x|, the precision of 3xTF32),
-                                 fp32 accumulate                                               */
-    LNERF_MFMA_BF16X6 = 512   /* fused path: the bf16x6 split (x = hi+mid+lo in bf16, six bf16
+                                 kernel runs: x 2^e = hi + lo in fp16 with per-sample (k1) or
+                                 per-layer slab (k2) and per-layer weight exponent shifts, three
+                                 fp16 MFMAs per product, fp32 accumulate. Each product drops
+                                 <= ~3 2^-22 of its operands' shifted magnitudes, i.e. relative to
+                                 max|w| max|x| of the shift group, not to |w x| itself (values far
+                                 below their group's maximum lose bits to fp16's subnormal range).
+                                 Requesting it where k16 cannot run (a head over 16 outputs,
+                                 LNERF_ONE_WAVE) is an error.                                  */
+    LNERF_MFMA_BF16X6 = 512,  /* fused path: the bf16x6 split (x = hi+mid+lo in bf16, six bf16
                                  MFMAs per product, dropped terms <= 2^-24 |w x|); the default
-                                 where k16 does not run (LNERF_K16=0, heads over 16 outputs) */
+                                 where k16 does not run (LNERF_ONE_WAVE, heads over 16 outputs) */
+    LNERF_ONE_WAVE = 1024     /* fused path: the one-wave-per-SIMD kernel pair
+                                 (fused_fwd_bwd_kernel + dw_all_kernel) instead of k16 + dw16,
+                                 for A/B runs; bf16x6 unless LNERF_MFMA_F32 / LNERF_MFMA_BF16.
+                                 At most one LNERF_MFMA_* precision flag may be set.            */
+};
+
+/* Engine options (lnerf_ctx_set_option). */
+enum {
+    LNERF_OPT_DW_GRID = 1     /* dW kernel workgroups per step (16..4096; 0 = the default 512) */
 };
 
 /* Optional outputs (device pointers; any may be NULL). */
@@ -187,17 +200,26 @@ int lnerf_render(lnerf_ctx* ctx, const lnerf_mlp* mlp, const float* ws, const fl
 int lnerf_ctx_timings(lnerf_ctx* ctx, float* ms_out, int n);
 
 /* Which kernels the last lnerf_train_step / lnerf_render on `ctx` ran (for tests and benches):
- * a mask of LNERF_PATH_* bits, the bf16 planes per operand of the fused MFMAs in bits 8-9
- * (3 = bf16x6 split, 1 = plain bf16, 0 = exact f32 or the generic path), or a negative error
- * code. 0 if no step has run. */
+ * a mask of LNERF_PATH_* bits, the operand planes of the fused MFMAs in bits 8-9 (3 = bf16x6
+ * split, 2 = fp16x3 split, 1 = plain bf16, 0 = exact f32 or the generic path), or a negative
+ * error code. 0 if no step has run. */
 enum {
     LNERF_PATH_GENERIC = 1,   /* the loma-order stage-by-stage kernels                        */
     LNERF_PATH_FUSED = 2,     /* the fused MFMA step (any kernel pair below)                  */
     LNERF_PATH_K16 = 4,       /* fused kernel on wave pairs (k16_fwd_bwd_kernel)              */
-    LNERF_PATH_DW16 = 8,      /* dW kernel on wave pairs (dw16_kernel)                        */
-    LNERF_PATH_KACT = 16      /* fused kernel with LDS-resident activations (kact_fwd_bwd_kernel) */
+    LNERF_PATH_DW16 = 8       /* dW kernel on wave pairs (dw16_kernel)                        */
 };
 int lnerf_ctx_last_path(lnerf_ctx* ctx);
+
+/* The hidden-layer ReLU decisions of the last training step on `ctx` (k16 path only, for parity
+ * tests: scripts/nerf.py:141-144 takes z > 0): `out` (device) receives (L-1) x R x 32 bytes, bit
+ * f % 8 of byte [(l R + r) 32 + f / 8] set when feature f of hidden layer l at sample row r was
+ * positive. Valid until the next call on `ctx`; an error after any other kind of call. */
+int lnerf_ctx_relu_masks(lnerf_ctx* ctx, unsigned char* out, size_t out_bytes, void* stream);
+
+/* Sets an engine option (LNERF_OPT_*) for later steps on `ctx`. Returns 0, or a negative code for
+ * an unknown option or an out-of-range value. */
+int lnerf_ctx_set_option(lnerf_ctx* ctx, int option, int value);
 
 /* buf[i] *= *scale for i < n (device pointers): applies a loss seed after an all-reduce of
  * unit-seeded gradients (the data-parallel path). */

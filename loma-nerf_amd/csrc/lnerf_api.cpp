@@ -17,6 +17,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "lnerf_internal.h"
@@ -103,10 +104,21 @@ struct CompatCtx {
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
-thread_local CompatCtx* tl_compat = nullptr;
+// One CompatCtx per calling thread, freed when that thread exits (its stream and staging go with
+// it). The main thread's context is left to process teardown: at exit() its thread_local
+// destructor may run after the HIP runtime has begun shutting down, where hipStreamDestroy is
+// not safe.
+const std::thread::id g_main_thread = std::this_thread::get_id();
+struct CompatHolder {
+    CompatCtx* ctx = nullptr;
+    ~CompatHolder() {
+        if (ctx && std::this_thread::get_id() != g_main_thread) delete ctx;
+    }
+};
+thread_local CompatHolder tl_compat;
 CompatCtx& compat() {
-    if (!tl_compat) tl_compat = new CompatCtx();
-    return *tl_compat;
+    if (!tl_compat.ctx) tl_compat.ctx = new CompatCtx();
+    return *tl_compat.ctx;
 }
 
 // Carves one contiguous region into float arrays (same offsets on host and device).
@@ -589,11 +601,24 @@ struct lnerf_ctx {
     hipEvent_t ev[7] = {};
     bool timed = false;
     int last_path = 0;   // lnerf_ctx_last_path
+    int dw_grid = 0;     // LNERF_OPT_DW_GRID (0: kDefaultDwGrid)
+    FusedPlan last_plan{};   // the last fused training step's plan (lnerf_ctx_relu_masks)
+    bool last_k16_train = false;
 };
 
 static int path_bits(const FusedPlan& p, bool train) {
-    return LNERF_PATH_FUSED | (p.kact ? LNERF_PATH_KACT : p.k16 ? LNERF_PATH_K16 : 0) |
-           (train && p.dw16 ? LNERF_PATH_DW16 : 0) | (p.x6 << 8);
+    return LNERF_PATH_FUSED | (p.k16 ? LNERF_PATH_K16 : 0) | (train && p.dw16 ? LNERF_PATH_DW16 : 0) |
+           (p.x6 << 8);
+}
+
+// At most one MFMA precision flag; fp16x3 only where k16 runs (it is k16's split).
+static void check_precision_flags(int flags) {
+    const int prec = flags & (LNERF_MFMA_F32 | LNERF_MFMA_BF16 | LNERF_MFMA_F16X3 | LNERF_MFMA_BF16X6);
+    if (prec & (prec - 1)) fail("conflicting MFMA precision flags 0x%x (set at most one)", prec);
+}
+static void check_plan_precision(const FusedPlan& p, int flags) {
+    if ((flags & LNERF_MFMA_F16X3) && p.x6 != 2)
+        fail("LNERF_MFMA_F16X3 needs the k16 kernel (head <= 16 outputs, no LNERF_ONE_WAVE)");
 }
 
 extern "C" const char* lnerf_last_error(void) { return g_last_error.c_str(); }
@@ -775,18 +800,23 @@ extern "C" int lnerf_train_step(lnerf_ctx* ctx, const lnerf_mlp* mlp, const floa
         if (!ws || !bs) fail("null weights");
         lnerf_outputs o = out ? *out : lnerf_outputs{};
         if (!(flags & LNERF_WANT_DX)) o.d_x = nullptr;
+        check_precision_flags(flags);
         std::lock_guard<std::mutex> lock(ctx->mu);
         HIP_OK(hipSetDevice(ctx->device));
         hipStream_t s = (hipStream_t)stream;   // NULL: the device's default (null) stream
         if (use_fused(*mlp, *batch, flags)) {
-            const size_t bytes = fused_workspace_bytes(*mlp, batch->rays, batch->samples);
+            const size_t bytes = fused_workspace_bytes(*mlp, batch->rays, batch->samples, true, ctx->dw_grid);
             FusedPlan p{};
-            fused_plan(p, *mlp, *batch, ctx->fused_ws.get(bytes), flags);
+            fused_plan(p, *mlp, *batch, ctx->fused_ws.get(bytes), flags, true, ctx->dw_grid);
+            check_plan_precision(p, flags);
             const bool timed = (flags & LNERF_TIMING) != 0;
             fused_train_step(p, ws, bs, *batch, seed, flags, o, s, timed ? ctx->ev : nullptr);
             ctx->timed = timed;
             ctx->last_path = path_bits(p, true);
+            ctx->last_plan = p;
+            ctx->last_k16_train = p.k16 != 0;
         } else {
+            ctx->last_k16_train = false;
             generic_step(ctx, *mlp, ws, bs, *batch, seed, flags, o, true, s);
             ctx->timed = false;
             ctx->last_path = LNERF_PATH_GENERIC;
@@ -811,16 +841,20 @@ extern "C" int lnerf_render(lnerf_ctx* ctx, const lnerf_mlp* mlp, const float* w
         if (!ctx) fail("null ctx");
         validate(mlp, batch);
         lnerf_outputs o = out ? *out : lnerf_outputs{};
+        check_precision_flags(flags);
         std::lock_guard<std::mutex> lock(ctx->mu);
         HIP_OK(hipSetDevice(ctx->device));
         hipStream_t s = (hipStream_t)stream;   // NULL: the device's default (null) stream
         if (use_fused(*mlp, *batch, flags & ~LNERF_WANT_DX)) {
-            const size_t bytes = fused_workspace_bytes(*mlp, batch->rays, batch->samples, false);
+            const size_t bytes = fused_workspace_bytes(*mlp, batch->rays, batch->samples, false, ctx->dw_grid);
             FusedPlan p{};
-            fused_plan(p, *mlp, *batch, ctx->fused_ws.get(bytes), flags, false);
+            fused_plan(p, *mlp, *batch, ctx->fused_ws.get(bytes), flags, false, ctx->dw_grid);
+            check_plan_precision(p, flags);
             fused_render(p, ws, bs, *batch, o, s);
             ctx->last_path = path_bits(p, false);
+            ctx->last_k16_train = false;
         } else {
+            ctx->last_k16_train = false;
             generic_step(ctx, *mlp, ws, bs, *batch, 1.0f, 0, o, false, s);
             ctx->last_path = LNERF_PATH_GENERIC;
         }
@@ -850,6 +884,35 @@ extern "C" int lnerf_ctx_last_path(lnerf_ctx* ctx) {
         path = ctx->last_path;
     });
     return rc != 0 ? rc : path;
+}
+
+extern "C" int lnerf_ctx_relu_masks(lnerf_ctx* ctx, unsigned char* out, size_t out_bytes, void* stream) {
+    return guard_int([&]() {
+        if (!ctx || !out) fail("null argument");
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        if (!ctx->last_k16_train) fail("no k16 training step has run on this context since the last other call");
+        const FusedPlan& p = ctx->last_plan;
+        const size_t need = (size_t)(p.L - 1) * p.R * 32;
+        if (out_bytes < need) fail("relu mask buffer holds %zu bytes, needs %zu", out_bytes, need);
+        HIP_OK(hipSetDevice(ctx->device));
+        k16_masks_launch(p, out, (hipStream_t)stream);
+        check_launch("lnerf_ctx_relu_masks");
+    });
+}
+
+extern "C" int lnerf_ctx_set_option(lnerf_ctx* ctx, int option, int value) {
+    return guard_int([&]() {
+        if (!ctx) fail("null ctx");
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        switch (option) {
+            case LNERF_OPT_DW_GRID:
+                if (value != 0 && (value < 16 || value > 4096)) fail("LNERF_OPT_DW_GRID %d outside 16..4096", value);
+                ctx->dw_grid = value;
+                break;
+            default:
+                fail("unknown option %d", option);
+        }
+    });
 }
 
 extern "C" int lnerf_scale_by_device_scalar(float* buf, size_t n, const float* scale, void* stream) {

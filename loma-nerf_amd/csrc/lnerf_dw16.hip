@@ -1,18 +1,21 @@
 // lnerf_dw16.hip -- k2 on wave pairs: dW_l = sum_s A_{l-1}[s]^T G_l[s] and db_l = sum_s G_l[s]
-// from the slabs k1 wrote, in k1's split (fp16x3 on v_mfma_f32_32x32x16_f16 with the slabs'
-// layer-wide exponent shifts, or bf16x6 on v_mfma_f32_32x32x16_bf16), two waves per SIMD.
+// from the slabs k1 wrote, in k1's split (fp16x3 on v_mfma_f32_32x32x16_f16 or bf16x6 on
+// v_mfma_f32_32x32x16_bf16, both with the slabs' layer-wide exponent shifts), two waves per SIMD.
 //
 // Reference: the weight/bias adjoints of nerf.py's reverse pass (reverse_diff.py:492-559;
 // dW_l += A_{l-1}^T G_l, db_l += sum_rows G_l). One workgroup (8 waves)
 // streams a contiguous range of 16-sample half-blocks of one layer:
-//  * global -> registers: the half-block's A rows (kt*32) and G rows (nt*32), 64 B per row, read
-//    as fully coalesced 16-B loads two half-blocks ahead (no LDS staging of fp32);
-//  * split once, cooperatively: every value is split into its hi/mid/lo bf16 planes exactly
-//    once per workgroup and written to a double-buffered LDS plane image [plane][row][16 samples]
-//    (the MFMA operand layout: 8 consecutive samples of a row = one 16-B fragment);
-//  * each wave owns a 64 x 128 block of the layer's output (2 x 4 tiles of 32 x 32, 128
-//    accumulator registers) and runs 6 MFMAs per tile pair and half-block;
-//  * db from the same registers (per-row partial sums, reduced in LDS at the end);
+//  * global -> registers: a slab tile's half-block is sample-major, [feature half 2][16 samples]
+//    [16 features] fp32 (the 1 KiB k1 writes with one global_store_dwordx4 per wave), read as
+//    fully coalesced 16-B loads (4 features of one sample per thread) three half-blocks ahead;
+//  * split once, cooperatively: every value is scaled and split into its hi/lo (fp16x3) or
+//    hi/mid/lo (bf16x6) planes exactly once per workgroup and written to a double-buffered LDS
+//    image [plane][16 samples][512 features] (A rows 0..255, G rows 256..511), 8 B per plane and
+//    thread (one ds_write_b64);
+//  * MFMA operands come out of that sample-major image transposed by ds_read_b64_tr_b16: lane
+//    (feature l & 31, samples 8 (l >> 5) ..+7) takes two 4-sample x 16-feature blocks;
+//  * each wave owns a TI x TJ block of 32 x 32 output tiles (2 x 4 for the hidden layers);
+//  * db from the same registers (per-feature partial sums, reduced in LDS at the end);
 //  * partials per split, summed in order by grad_reduce_kernel (deterministic, no atomics).
 #include "lnerf_internal.h"
 
@@ -37,8 +40,12 @@ typedef _Float16 hf4 __attribute__((ext_vector_type(4)));
 
 constexpr int kThreads = 512;
 constexpr int kRows = 512;                  // A rows [0, 256) and G rows [256, 512) of the image
-constexpr int kPlaneBytes = kRows * 32;     // one plane of a half-block: [row][16 samples] 16-bit
-// PL planes per operand: 3 = bf16x6, 2 = fp16x3 (x 2^e = hi + lo, the slab's layer-wide shift)
+// one plane of a half-block: [16 samples][512 features] 16-bit, each sample's row padded by 64 B
+// so that the 4 sample rows one ds_read_b64_tr_b16 lane group reads start 16 banks apart
+// (conflict-free reads; the ds_write_b64 image writes see a 2-way conflict)
+constexpr int kImgRow = kRows * 2 + 64;
+constexpr int kPlaneBytes = 16 * kImgRow;
+// PL planes per operand: 3 = bf16x6, 2 = fp16x3, 1 = bf16 (all split x 2^e, per-sample shifts)
 template <int PL>
 constexpr int image_bytes() { return PL * kPlaneBytes; }
 
@@ -57,36 +64,29 @@ struct Dw16Args {
     size_t dwp_off[kMaxLayers];
     float* db_part;
     size_t dbp_off[kMaxLayers];
-    const int* smax;            // PL = 2: slab max bits, [l] layer l's input, [L + l] G_l
+    const unsigned short* sexp; // k1's per-sample shifts [l][position]: byte 0 A_{l-1}, byte 1 G_l
+    int rpad;                   // slab positions per layer
+    const int* eshift;          // per-layer product shift E_l (k1_reduce_kernel)
     int L;
 };
 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
-// the exponent shift e with max 2^e in [2^13, 2^14) from a slab max's bits (0: zero/non-finite)
-__device__ __forceinline__ int shift_of_bits(int bits) {
-    const float m = __int_as_float(bits);
-    if (!(m > 0.0f) || !(m < __builtin_inff())) return 0;
-    int e;
-    (void)__builtin_frexpf(m, &e);
-    return 14 - e;
-}
-
-// The 16 B that thread t loads in round i (0..3) of a half-block: image row r = 128 i + t / 4
-// (rounds 0, 1: A rows; 2, 3: G rows), samples 4 (t % 4) .. +3. A slab block is
-// [tile][half][32 rows][16 samples]; a half-block is one half of one 32-sample block. The
+// The 16 B that thread t loads in round i (0..3) of a half-block: rounds 0, 1 are A tiles 0-3 and
+// 4-7, rounds 2, 3 G tiles 0-3 and 4-7; tile 4 (i & 1) + t / 128, and inside the tile's 512-float
+// half-block [h][n][16 f] the floats 4 (t % 128) ..+3 = features 16 h + 4 (t % 4) ..+3 of sample
+// n, with h = (t / 64) % 2 and n = (t % 64) / 4. A slab block is [tile][half-block 2][512]. The
 // per-thread part of the offset is fixed (RowMap), the half-block part is wave-uniform.
 struct RowMap {
-    int lane;        // per-thread float offset inside a tile's half: row (t/4) % 32, samples 4 (t % 4)
-    int tile[4];     // wave-uniform: the 32-row tile of round i (tile 0 for rows past the layer)
-    bool ok[4];      // wave-uniform: the row exists in this layer (else it is never split)
+    int lane;        // per-thread float offset inside a tile's half-block: 4 (t % 128)
+    int tile[4];     // wave-uniform: the 32-feature tile of round i (tile 0 for tiles past the layer)
+    bool ok[4];      // wave-uniform: the tile exists in this layer (else it is never split)
 };
 
 __device__ __forceinline__ RowMap row_map(int kt, int nt) {
     RowMap m;
     const int t = threadIdx.x;
-    m.lane = ((t >> 2) & 31) * 16 + 4 * (t & 3);
-    // a round's 16 rows of a wave lie in one tile: tile = (128 (i & 1) + t / 4) / 32 = 4 (i & 1) + wave / 2
+    m.lane = 4 * (t & 127);
     const int w2 = wave_id() >> 1;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -97,17 +97,45 @@ __device__ __forceinline__ RowMap row_map(int kt, int nt) {
     return m;
 }
 
+// image feature row of round i's 4 values for thread t (A rows 0..255, G rows 256..511)
+__device__ __forceinline__ int image_row(int i) {
+    const int t = threadIdx.x;
+    return (i < 2 ? 0 : 256) + 32 * (4 * (i & 1) + (t >> 7)) + 16 * ((t >> 6) & 1) + 4 * (t & 3);
+}
+
 struct Loads {
     fx4 v[4];
+    unsigned e;   // the sample's k1 shifts: byte 0 its A row's, byte 1 its G row's (int8)
 };
+
+// Per-sample balancing of the split: the product of a sample's A row and G row is what dW sums,
+// so a sample's A row is scaled by 2^ea and its G row by 2^eg with ea + eg = E_l for every sample
+// (E_l = min over samples of exA + exG, the row shifts k1 used; k1_reduce_kernel): the products
+// keep one layer-wide scale while each operand sits within D/2 binades of its own ideal shift,
+// D = exA + exG - E_l -- a sample whose A is tiny and G huge (tiny sigma behind the 1e8 delta)
+// no longer pushes every other sample's G toward fp16's subnormals. Neither operand exceeds its
+// own ideal shift, so nothing overflows. -128 marks an all-zero row: its partner keeps its own
+// shift (the zero products stay zero).
+__device__ __forceinline__ void sample_shifts(unsigned e, int E, int& ea, int& eg) {
+    const int xa = (int)(signed char)(e & 0xFFu), xg = (int)(signed char)(e >> 8);
+    if (xa == -128 || xg == -128) {
+        ea = xa == -128 ? 0 : xa;
+        eg = xg == -128 ? 0 : xg;
+        return;
+    }
+    const int d = xa + xg - E;   // >= 0
+    ea = xa - (d >> 1);
+    eg = xg - ((d + 1) >> 1);
+}
 
 // Always four loads from valid addresses and no select on the data (nothing waits for it before
 // its use): rows past the layer's tiles are never split, half-blocks past the split land in the
 // idle image and add nothing to db (the callers' hb < hb1 guards).
-__device__ __forceinline__ void issue_loads(const float* A, const float* G, int kt, int nt, const RowMap& m,
-                                            int hb, int hb_end, Loads& L) {
+__device__ __forceinline__ void issue_loads(const float* A, const float* G, const unsigned short* se, int kt,
+                                            int nt, const RowMap& m, int hb, int hb_end, Loads& L) {
     const bool in = hb < hb_end;
     const int hbc = in ? hb : max(0, hb_end - 1);
+    L.e = se[hbc * 16 + ((threadIdx.x & 63) >> 2)];
     const int blk = hbc >> 1, half = hbc & 1;
     const float* pa = A + (size_t)blk * kt * 1024 + half * 512;
     const float* pg = G + (size_t)blk * nt * 1024 + half * 512;
@@ -142,16 +170,15 @@ __device__ __forceinline__ void split_h2(float x0, float x1, float sc, unsigned&
         : "+v"(lo) : "v"(x1), "v"(sc), "v"(hi));
 }
 
-// Split round i of the thread's values into the plane image (8 B per plane and row); rounds 0, 1
-// are A rows (shift ea), 2, 3 G rows (shift eg).
+// Split round i of the thread's values (4 features of sample n) into the plane image: 8 B per
+// plane at [plane][n][row .. row + 3]; rounds 0, 1 are A rows (shift ea), 2, 3 G rows (shift eg).
 template <int PL>
-__device__ __forceinline__ void write_planes_row(const fx4& v, int i, unsigned char* img, int ea, int eg) {
-    const int t = threadIdx.x, q = t & 3;
-    const int r = 128 * i + (t >> 2);
-    unsigned char* p = img + r * 32 + q * 8;
+__device__ __forceinline__ void write_planes_row(const fx4& v, int i, unsigned char* img, float sa, float sg) {
+    const int t = threadIdx.x;
+    unsigned char* p = img + ((t & 63) >> 2) * kImgRow + image_row(i) * 2;
+    const float sc = i < 2 ? sa : sg;
     if constexpr (PL == 2) {
         typedef unsigned u2 __attribute__((ext_vector_type(2)));
-        const float sc = __builtin_ldexpf(1.0f, i < 2 ? ea : eg);
         unsigned h0, l0, h1, l1;
         split_h2(v[0], v[1], sc, h0, l0);
         split_h2(v[2], v[3], sc, h1, l1);
@@ -159,17 +186,27 @@ __device__ __forceinline__ void write_planes_row(const fx4& v, int i, unsigned c
         *(u2*)(p + kPlaneBytes) = u2{l0, l1};
     } else {
         bf4 h, m, lo;
-        split4(v, h, m, lo);
+        split4(v * sc, h, m, lo);
         *(bf4*)(p) = h;
         *(bf4*)(p + kPlaneBytes) = m;
         *(bf4*)(p + 2 * kPlaneBytes) = lo;
     }
 }
 
+// the split scales 2^ea (A rows) and 2^eg (G rows) of a half-block's sample (sample_shifts)
+__device__ __forceinline__ void sample_scales(unsigned e, int E, float& sa, float& sg) {
+    int ea, eg;
+    sample_shifts(e, E, ea, eg);
+    sa = __builtin_ldexpf(1.0f, ea);
+    sg = __builtin_ldexpf(1.0f, eg);
+}
+
 template <int PL>
-__device__ __forceinline__ void write_planes(const Loads& L, unsigned char* img, int ea, int eg) {
+__device__ __forceinline__ void write_planes(const Loads& L, unsigned char* img, int E) {
+    float sa, sg;
+    sample_scales(L.e, E, sa, sg);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) write_planes_row<PL>(L.v[i], i, img, ea, eg);
+    for (int i = 0; i < 4; ++i) write_planes_row<PL>(L.v[i], i, img, sa, sg);
 }
 
 __device__ __forceinline__ fx16 mfma32(const bf8& a, const bf8& b, fx16 c) {
@@ -180,34 +217,56 @@ __device__ __forceinline__ fx16 mfma32h(const bf8& a, const bf8& b, fx16 c) {
                                                   0);
 }
 
-// The wave's TI x TJ tile block (TI 32-row tiles of A, TJ of G) on one half-block image (per
-// tile a fragment is one ds_read_b128 per plane; lane: row l & 31, samples 8 (l >> 5) .. +7),
-// with the split of the next half-block interleaved (round k beside output column tile k), so
-// the VALU split issues under the MFMAs. Branch-free (ACTIVE is a template parameter; past the
+typedef short s4 __attribute__((ext_vector_type(4)));
+
+// One MFMA operand fragment (32 features x 16 samples, one plane) from the sample-major image:
+// two ds_read_b64_tr_b16, samples 8 h .. +3 and 8 h + 4 .. +7 of lane l's feature (h = l >> 5).
+// `addr` is this lane's byte address of the fragment's first feature in the plane.
+__device__ __forceinline__ bf8 read_frag(unsigned char* addr) {
+    typedef __attribute__((address_space(3))) s4* lp;
+    const s4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(__attribute__((address_space(3))) void*)addr);
+    const s4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lp)(__attribute__((address_space(3))) void*)(addr + 4 * kImgRow));
+    typedef short s8 __attribute__((ext_vector_type(8)));
+    return __builtin_bit_cast(bf8, s8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]});
+}
+
+// This lane's byte offset inside a plane for a fragment starting at feature 0: lane 4 q + p of
+// each 16-lane group supplies sample row 8 (l >> 5) + q, features 16 ((l >> 4) & 1) + 4 p ..+3
+// (ds_read_b64_tr_b16 hands lane i of the group feature i of the 4 rows).
+__device__ __forceinline__ int frag_lane_off() {
+    const int l = threadIdx.x & 63;
+    return (8 * (l >> 5) + ((l >> 2) & 3)) * kImgRow + (16 * ((l >> 4) & 1) + 4 * (l & 3)) * 2;
+}
+
+// The wave's TI x TJ tile block (TI 32-row tiles of A, TJ of G) on one half-block image, with
+// the split of the next half-block interleaved (round k beside output column tile k), so the
+// VALU split issues under the MFMAs. Branch-free (ACTIVE is a template parameter; past the
 // split's last half-block the zeroed loads land in the idle image buffer).
 template <int PL, int TI, int TJ, bool ACTIVE, bool FULL>
 __device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int g0, fx16 (&acc)[TI][TJ],
-                                          const Loads& nl, unsigned char* nxt, const RowMap& m, int ea,
-                                          int eg) {
-    const int lane = threadIdx.x & 63, fo = (lane & 31) * 32 + (lane >> 5) * 16;
+                                          const Loads& nl, unsigned char* nxt, const RowMap& m, int E) {
+    float sa, sg;
+    sample_scales(nl.e, E, sa, sg);
+    unsigned char* fl = (unsigned char*)img + frag_lane_off();
     bf8 ap[TI][PL];
     if constexpr (ACTIVE) {
 #pragma unroll
         for (int i = 0; i < TI; ++i)
 #pragma unroll
-            for (int p = 0; p < PL; ++p) ap[i][p] = *(const bf8*)(img + p * kPlaneBytes + (a0 + 32 * i) * 32 + fo);
+            for (int p = 0; p < PL; ++p) ap[i][p] = read_frag(fl + p * kPlaneBytes + (a0 + 32 * i) * 2);
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         // rows past the layer's tiles are never read: skip their split (wave-uniform: a wave's
-        // 16 rows of a round lie in one 32-row tile); FULL layers need no branch
-        if (FULL || m.ok[k]) write_planes_row<PL>(nl.v[k], k, nxt, ea, eg);
+        // values of a round lie in one 32-feature tile); FULL layers need no branch
+        if (FULL || m.ok[k]) write_planes_row<PL>(nl.v[k], k, nxt, sa, sg);
         if constexpr (ACTIVE) {
             if (k < TJ) {
                 const int j = k < TJ ? k : 0;
                 bf8 gp[PL];
 #pragma unroll
-                for (int p = 0; p < PL; ++p) gp[p] = *(const bf8*)(img + p * kPlaneBytes + (256 + g0 + 32 * j) * 32 + fo);
+                for (int p = 0; p < PL; ++p) gp[p] = read_frag(fl + p * kPlaneBytes + (256 + g0 + 32 * j) * 2);
 #pragma unroll
                 for (int i = 0; i < TI; ++i) {
                     fx16 c = acc[i][j];
@@ -215,6 +274,8 @@ __device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int 
                         c = mfma32h(ap[i][0], gp[1], c);   // small terms first
                         c = mfma32h(ap[i][1], gp[0], c);
                         c = mfma32h(ap[i][0], gp[0], c);
+                    } else if constexpr (PL == 1) {
+                        c = mfma32(ap[i][0], gp[0], c);
                     } else {
                         c = mfma32(ap[i][0], gp[2], c);   // small terms first
                         c = mfma32(ap[i][1], gp[1], c);
@@ -230,66 +291,41 @@ __device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int 
     }
 }
 
-// The half-block loop of one split: L0 holds hb0 (already in the image), L1 hb0 + 1.
-template <int PL, int TI, int TJ, bool ACTIVE, bool FULL>
-__device__ __forceinline__ void hb_loop(const float* A, const float* G, int kt, int nt, const RowMap& m,
-                                        int hb0, int hb1, int a0, int g0, fx16 (&acc)[TI][TJ], Loads& L0,
-                                        Loads& L1, float (&dbs)[2], unsigned char* lds, int ea, int eg) {
-    constexpr int kIB = image_bytes<PL>();
-    for (int hb = hb0; hb < hb1; ++hb) {
-        const int cur = (hb - hb0) & 1;
-        // L1 holds hb + 1; L0 receives hb + 2
-        issue_loads(A, G, kt, nt, m, hb + 2, hb1, L0);
-        if (hb + 1 < hb1) {
-            dbs[0] += (L1.v[2][0] + L1.v[2][1]) + (L1.v[2][2] + L1.v[2][3]);
-            dbs[1] += (L1.v[3][0] + L1.v[3][1]) + (L1.v[3][2] + L1.v[3][3]);
-        }
-        block_mma<PL, TI, TJ, ACTIVE, FULL>(lds + cur * kIB, a0, g0, acc, L1, lds + (cur ^ 1) * kIB, m, ea, eg);
-        __syncthreads();
-        Loads t = L0;
-        L0 = L1;
-        L1 = t;
-    }
-}
-
-// Three half-blocks in flight (LNERF_DW16_DEPTH=3): step I of a 3-step rotation over the load
+// Three half-blocks in flight: step I of a 3-step rotation over the load
 // register sets (images alternate at run time). Entering half-block hb: its planes are in image
 // (hb - hb0) & 1, the set after I holds hb + 1 (split now into the other image), the one after
 // that hb + 2 (in flight) and set I is free: it receives hb + 3.
-#ifndef LNERF_DW16_DEPTH
-#define LNERF_DW16_DEPTH 3
-#endif
 template <int PL, int TI, int TJ, bool ACTIVE, bool FULL, int I>
-__device__ __forceinline__ void hb_step3(const float* A, const float* G, int kt, int nt, const RowMap& m, int hb,
-                                         int hb0, int hb1, int a0, int g0, fx16 (&acc)[TI][TJ], Loads& L0,
-                                         Loads& L1, Loads& L2, float (&dbs)[2], unsigned char* lds, int ea,
-                                         int eg) {
+__device__ __forceinline__ void hb_step3(const float* A, const float* G, const unsigned short* se, int kt, int nt,
+                                         const RowMap& m, int hb, int hb0, int hb1, int a0, int g0,
+                                         fx16 (&acc)[TI][TJ], Loads& L0, Loads& L1, Loads& L2, fx4 (&dbs)[2],
+                                         unsigned char* lds, int E) {
     constexpr int kIB = image_bytes<PL>();
     Loads& fr = I == 0 ? L0 : I == 1 ? L1 : L2;
     const Loads& nx = I == 0 ? L1 : I == 1 ? L2 : L0;
-    issue_loads(A, G, kt, nt, m, hb + 3, hb1, fr);
+    issue_loads(A, G, se, kt, nt, m, hb + 3, hb1, fr);
     if (hb + 1 < hb1) {
-        dbs[0] += (nx.v[2][0] + nx.v[2][1]) + (nx.v[2][2] + nx.v[2][3]);
-        dbs[1] += (nx.v[3][0] + nx.v[3][1]) + (nx.v[3][2] + nx.v[3][3]);
+        dbs[0] += nx.v[2];
+        dbs[1] += nx.v[3];
     }
     const int cur = (hb - hb0) & 1;
-    block_mma<PL, TI, TJ, ACTIVE, FULL>(lds + cur * kIB, a0, g0, acc, nx, lds + (cur ^ 1) * kIB, m, ea, eg);
+    block_mma<PL, TI, TJ, ACTIVE, FULL>(lds + cur * kIB, a0, g0, acc, nx, lds + (cur ^ 1) * kIB, m, E);
     __syncthreads();
 }
 
 template <int PL, int TI, int TJ, bool ACTIVE, bool FULL>
-__device__ __forceinline__ void hb_loop3(const float* A, const float* G, int kt, int nt, const RowMap& m,
-                                         int hb0, int hb1, int a0, int g0, fx16 (&acc)[TI][TJ], Loads& L0,
-                                         Loads& L1, Loads& L2, float (&dbs)[2], unsigned char* lds, int ea,
-                                         int eg) {
+__device__ __forceinline__ void hb_loop3(const float* A, const float* G, const unsigned short* se, int kt, int nt,
+                                         const RowMap& m, int hb0, int hb1, int a0, int g0, fx16 (&acc)[TI][TJ],
+                                         Loads& L0, Loads& L1, Loads& L2, fx4 (&dbs)[2], unsigned char* lds,
+                                         int E) {
     int hb = hb0;
     for (; hb + 3 <= hb1; hb += 3) {
-        hb_step3<PL, TI, TJ, ACTIVE, FULL, 0>(A, G, kt, nt, m, hb, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, ea, eg);
-        hb_step3<PL, TI, TJ, ACTIVE, FULL, 1>(A, G, kt, nt, m, hb + 1, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, ea, eg);
-        hb_step3<PL, TI, TJ, ACTIVE, FULL, 2>(A, G, kt, nt, m, hb + 2, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, ea, eg);
+        hb_step3<PL, TI, TJ, ACTIVE, FULL, 0>(A, G, se, kt, nt, m, hb, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
+        hb_step3<PL, TI, TJ, ACTIVE, FULL, 1>(A, G, se, kt, nt, m, hb + 1, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
+        hb_step3<PL, TI, TJ, ACTIVE, FULL, 2>(A, G, se, kt, nt, m, hb + 2, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
     }
-    if (hb < hb1) hb_step3<PL, TI, TJ, ACTIVE, FULL, 0>(A, G, kt, nt, m, hb, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, ea, eg);
-    if (hb + 1 < hb1) hb_step3<PL, TI, TJ, ACTIVE, FULL, 1>(A, G, kt, nt, m, hb + 1, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, ea, eg);
+    if (hb < hb1) hb_step3<PL, TI, TJ, ACTIVE, FULL, 0>(A, G, se, kt, nt, m, hb, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
+    if (hb + 1 < hb1) hb_step3<PL, TI, TJ, ACTIVE, FULL, 1>(A, G, se, kt, nt, m, hb + 1, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
 }
 
 // One split of layer l with TI x TJ tile blocks per wave (the layer's ceil(KT/TI) x ceil(NT/TJ)
@@ -311,46 +347,31 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
     for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j) acc[i][j] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    // db: this thread's G rows are image rows 128 i + t/4 for i = 2, 3 (4 samples each)
-    float dbs[2] = {0.0f, 0.0f};
+    // db: this thread's G values are features image_row(i) - 256 ..+3 of one sample, i = 2, 3
+    fx4 dbs[2] = {fx4{0.0f, 0.0f, 0.0f, 0.0f}, fx4{0.0f, 0.0f, 0.0f, 0.0f}};
 
     const float* A = a.act + a.a_off[l];
     const float* G = a.grad + a.g_off[l];
     const RowMap m = row_map(KT, NT);
-    // PL = 2: the layer-wide exponent shifts of the A_{l-1} and G_l slabs (k1's slab maxima); the
-    // partials are shifted back by -(ea + eg) (exact)
-    const int ea = PL == 2 ? shift_of_bits(a.smax[l]) : 0, eg = PL == 2 ? shift_of_bits(a.smax[a.L + l]) : 0;
+    // the per-sample balanced shifts (sample_shifts): every product carries 2^E, removed from the
+    // partials at the end (exact)
+    const unsigned short* se = a.sexp + (size_t)l * a.rpad;
+    const int E = a.eshift[l];
     const bool full = KT == 8 && NT == 8;
-    if constexpr (LNERF_DW16_DEPTH == 3) {
-        Loads L0, L1, L2;
-        issue_loads(A, G, KT, NT, m, hb0, hb1, L0);
-        issue_loads(A, G, KT, NT, m, hb0 + 1, hb1, L1);
-        issue_loads(A, G, KT, NT, m, hb0 + 2, hb1, L2);
-        if (hb0 < hb1) {
-            dbs[0] += (L0.v[2][0] + L0.v[2][1]) + (L0.v[2][2] + L0.v[2][3]);
-            dbs[1] += (L0.v[3][0] + L0.v[3][1]) + (L0.v[3][2] + L0.v[3][3]);
-            write_planes<PL>(L0, lds, ea, eg);
-        }
-        __syncthreads();
-        if (active && full) hb_loop3<PL, TI, TJ, true, true>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, ea, eg);
-        else if (active) hb_loop3<PL, TI, TJ, true, false>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, ea, eg);
-        else if (full) hb_loop3<PL, TI, TJ, false, true>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, ea, eg);
-        else hb_loop3<PL, TI, TJ, false, false>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, ea, eg);
-    } else {
-        Loads L0, L1;
-        issue_loads(A, G, KT, NT, m, hb0, hb1, L0);
-        issue_loads(A, G, KT, NT, m, hb0 + 1, hb1, L1);
-        if (hb0 < hb1) {
-            dbs[0] += (L0.v[2][0] + L0.v[2][1]) + (L0.v[2][2] + L0.v[2][3]);
-            dbs[1] += (L0.v[3][0] + L0.v[3][1]) + (L0.v[3][2] + L0.v[3][3]);
-            write_planes<PL>(L0, lds, ea, eg);
-        }
-        __syncthreads();
-        if (active && full) hb_loop<PL, TI, TJ, true, true>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, ea, eg);
-        else if (active) hb_loop<PL, TI, TJ, true, false>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, ea, eg);
-        else if (full) hb_loop<PL, TI, TJ, false, true>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, ea, eg);
-        else hb_loop<PL, TI, TJ, false, false>(A, G, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, ea, eg);
+    Loads L0, L1, L2;
+    issue_loads(A, G, se, KT, NT, m, hb0, hb1, L0);
+    issue_loads(A, G, se, KT, NT, m, hb0 + 1, hb1, L1);
+    issue_loads(A, G, se, KT, NT, m, hb0 + 2, hb1, L2);
+    if (hb0 < hb1) {
+        dbs[0] += L0.v[2];
+        dbs[1] += L0.v[3];
+        write_planes<PL>(L0, lds, E);
     }
+    __syncthreads();
+    if (active && full) hb_loop3<PL, TI, TJ, true, true>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
+    else if (active) hb_loop3<PL, TI, TJ, true, false>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
+    else if (full) hb_loop3<PL, TI, TJ, false, true>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
+    else hb_loop3<PL, TI, TJ, false, false>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
 
     // partial [split][k][j], k < KT*32, j < NT*32 (32x32 C/D layout: row (r&3)+8(r>>2)+4h, col l&31)
     if (active) {
@@ -366,19 +387,25 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
                     for (int r = 0; r < 16; ++r) {
                         const int k = kb + (r & 3) + 8 * (r >> 2) + 4 * h;
                         part[(size_t)k * ncol + jb + (lane & 31)] =
-                            PL == 2 ? __builtin_ldexpf(acc[i][j][r], -(ea + eg)) : acc[i][j][r];
+                            __builtin_ldexpf(acc[i][j][r], -E);
                     }
                 }
             }
     }
-    // db: 4 threads per G row -> in-order sum through LDS
+    // db: 16 threads (one per sample n) per G feature -> in-order sum through LDS [feature][n]
     float* red = (float*)lds;
+    __syncthreads();   // the image buffers are free: every wave is past its last MFMA reads
 #pragma unroll
-    for (int i = 0; i < 2; ++i) red[(i * 128 + (tid >> 2)) * 4 + (tid & 3)] = dbs[i];
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[(image_row(2 + i) - 256 + j) * 16 + ((tid & 63) >> 2)] = dbs[i][j];
     __syncthreads();
     if (tid < NT * 32) {
-        const float* q = red + tid * 4;
-        a.db_part[a.dbp_off[l] + (size_t)sp * NT * 32 + tid] = (q[0] + q[1]) + (q[2] + q[3]);
+        const float* q = red + tid * 16;
+        float s0 = 0.0f;
+#pragma unroll
+        for (int n = 0; n < 16; ++n) s0 += q[n];
+        a.db_part[a.dbp_off[l] + (size_t)sp * NT * 32 + tid] = s0;
     }
 }
 
@@ -404,35 +431,29 @@ __global__ void __launch_bounds__(kThreads, 1) dw16_kernel(Dw16Args a) {
 }
 
 // The reductions between k1 and dw16 in one launch (1024 threads per block):
-//  * blocks [0, nslab): PL = 2, slab b's layer-wide max from k1's per-wave maxima (n per slab), as
-//    the bits of a non-negative float in smax[b] (the exponent shifts dw16 splits with);
-//  * block nslab: the batch loss, the same deterministic 256-lane tree as loss_reduce_kernel
+//  * blocks [0, nl): layer l's product shift E_l = min over samples of exA + exG (k1's per-sample
+//    shifts of the layer's A and G rows), from k1's per-wave minima (n per layer; all-zero rows
+//    excluded; 0 if every row is), the scale dw16's per-sample balancing keeps uniform;
+//  * block nl: the batch loss, the same deterministic 256-lane tree as loss_reduce_kernel
 //    (lnerf_fused.hip), into *total (the loss seed) and *out_loss.
-__global__ void __launch_bounds__(1024) k1_reduce_kernel(const float* __restrict__ part, int n,
-                                                         int* __restrict__ smax, int nslab,
+__global__ void __launch_bounds__(1024) k1_reduce_kernel(const int* __restrict__ epart, int n,
+                                                         int* __restrict__ eshift, int nl,
                                                          const float* __restrict__ loss_part, int nwg,
                                                          float* total, float* out_loss) {
     __shared__ float red[1024];
     const int t = threadIdx.x;
-    if ((int)blockIdx.x < nslab) {
-        const float* q = part + (size_t)blockIdx.x * n;
-        float m = 0.0f;
-        if ((n & 3) == 0) {
-            const float4* q4 = reinterpret_cast<const float4*>(q);
-            for (int i = t; i < (n >> 2); i += 1024) {
-                const float4 v = q4[i];
-                m = fmaxf(fmaxf(m, fmaxf(v.x, v.y)), fmaxf(v.z, v.w));
-            }
-        } else {
-            for (int i = t; i < n; i += 1024) m = fmaxf(m, q[i]);
-        }
-        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-        if ((t & 63) == 0) red[t >> 6] = m;
+    if ((int)blockIdx.x < nl) {
+        const int* q = epart + (size_t)blockIdx.x * n;
+        int m = 1 << 20;
+        for (int i = t; i < n; i += 1024) m = min(m, q[i]);
+        for (int o = 32; o > 0; o >>= 1) m = min(m, __shfl_xor(m, o));
+        int* ired = (int*)red;
+        if ((t & 63) == 0) ired[t >> 6] = m;
         __syncthreads();
         if (t == 0) {
-            float r = red[0];
-            for (int w = 1; w < 16; ++w) r = fmaxf(r, red[w]);
-            smax[blockIdx.x] = __float_as_int(r);
+            int r = ired[0];
+            for (int w = 1; w < 16; ++w) r = min(r, ired[w]);
+            eshift[blockIdx.x] = r == (1 << 20) ? 0 : r;
         }
         return;
     }
@@ -473,17 +494,20 @@ void dw16_launch(const FusedPlan& p, hipStream_t s) {
     a.blocks = p.blocks;
     a.dw_part = p.dw_part;
     a.db_part = p.db_part;
-    a.smax = p.smax16;
+    a.sexp = (const unsigned short*)p.sexp;
+    a.rpad = p.num_wg * 128;
+    a.eshift = p.dw_shift;
     a.L = p.L;
-    // PL = 2 needs the slab maxima of k1_reduce_launch (launched right after k1)
+    // the per-layer product shifts of k1_reduce_launch (launched right after k1)
     if (p.x6 == 2) dw16_kernel<2><<<p.dw_grid, kThreads, 0, s>>>(a);
-    else dw16_kernel<3><<<p.dw_grid, kThreads, 0, s>>>(a);
+    else if (p.x6 == 3) dw16_kernel<3><<<p.dw_grid, kThreads, 0, s>>>(a);
+    else dw16_kernel<1><<<p.dw_grid, kThreads, 0, s>>>(a);
 }
 
 void k1_reduce_launch(const FusedPlan& p, float* out_loss, hipStream_t s) {
-    const int nslab = (p.dw16 && p.x6 == 2) ? 2 * p.L : 0;
-    k1_reduce_kernel<<<nslab + 1, 1024, 0, s>>>(p.smax_part, p.num_wg * 8, p.smax16, nslab, p.loss_part,
-                                                p.num_wg, p.loss_total, out_loss);
+    const int nl = p.dw16 ? p.L : 0;
+    k1_reduce_kernel<<<nl + 1, 1024, 0, s>>>(p.epart, p.num_wg * 8, p.dw_shift, nl, p.loss_part, p.num_wg,
+                                             p.loss_total, out_loss);
 }
 
 }  // namespace lnerf

@@ -1486,7 +1486,7 @@ struct Layout {
 inline int pow2_tiles(int t) { return t <= 1 ? 1 : t <= 2 ? 2 : t <= 4 ? 4 : 8; }
 
 // train = false (render): no slabs or dW partials (the forward-only kernel writes none).
-void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S, bool train = true) {
+void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S, bool train, int dw_grid) {
     const int L = m.num_layers;
     int kt[kMaxLayers], nt[kMaxLayers];
     for (int l = 0; l < L; ++l) {
@@ -1546,19 +1546,11 @@ void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S, bool train = tr
     off = 0;
     for (int l = 0; l < L; ++l) { y.grad_off[l] = off; off += (size_t)y.blocks * nt[l] * 1024; }
     y.grad_total = train ? off : 0;
-    // dW: one launch over every layer (dw_all_kernel), ~kDwGrid workgroups split between the
-    // layers in proportion to the slab bytes each one streams (kt + nt tiles per 32-sample
-    // block): the kernel is bandwidth-bound, so equal bytes per workgroup balance it. Phased
-    // (small) layers write 4 partials per split.
-    // (LNERF_DW_GRID overrides the workgroup budget for A/B runs: read once, clamped to
-    // [16, 4096]; an unparsable value keeps the default)
-    static const int kDwGrid = [] {
-        const char* eg = getenv("LNERF_DW_GRID");
-        char* end = nullptr;
-        const long v = eg ? strtol(eg, &end, 10) : 0;
-        if (!eg || end == eg || *end != '\0') return 512;
-        return (int)(v < 16 ? 16 : v > 4096 ? 4096 : v);
-    }();
+    // dW: one launch over every layer, ~dw_grid workgroups (lnerf_ctx_set_option
+    // LNERF_OPT_DW_GRID; 512 by default) split between the layers in proportion to the slab bytes
+    // each one streams (kt + nt tiles per 32-sample block): the kernel is bandwidth-bound, so
+    // equal bytes per workgroup balance it. Phased (small) layers write 4 partials per split.
+    const int kDwGrid = dw_grid > 0 ? (dw_grid < 16 ? 16 : dw_grid > 4096 ? 4096 : dw_grid) : kDefaultDwGrid;
     size_t dwp = 0, dbp = 0;
     int tiles_sum = 0;
     for (int l = 0; l < L; ++l) {
@@ -1606,31 +1598,31 @@ bool fused_supported(const lnerf_mlp& m, int rays, int S, int input_mode, const 
     return w == nullptr;
 }
 
-size_t fused_workspace_bytes(const lnerf_mlp& m, int rays, int S, bool train) {
+size_t fused_workspace_bytes(const lnerf_mlp& m, int rays, int S, bool train, int dw_grid) {
     Layout y;
-    make_layout(y, m, rays, S, train);
+    make_layout(y, m, rays, S, train, dw_grid);
     size_t f = align_up(y.pack_total, 64) + align_up((y.w6_total + 1) / 2, 64) +
                align_up(y.act_total, 64) + align_up(y.grad_total, 64) +
                align_up((size_t)y.num_wg, 64) + align_up(y.dwp_total, 64) + align_up(y.dbp_total, 64) +
                64 + align_up((y.w16_total + 1) / 2, 64) + align_up(y.b16_total, 64) +
                align_up(y.mask_total * 2, 64) + 64 +   // + the fp16x3 weight/slab maxima
                align_up((size_t)kMaxLayers * kWmaxParts, 64) +   // + per-block max|W| partials
-               (train ? align_up((size_t)2 * m.num_layers * y.num_wg * 8, 64) : 0);
+               (train ? align_up((size_t)m.num_layers * y.num_wg * 64, 64) +      // per-sample shifts
+                            align_up((size_t)m.num_layers * y.num_wg * 8, 64) : 0);   // per-wave minima
     return f * sizeof(float);
 }
 
 void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws_base, int flags,
-                bool train) {
+                bool train, int dw_grid) {
     Layout y;
-    make_layout(y, m, b.rays, b.samples, train);
+    make_layout(y, m, b.rays, b.samples, train, dw_grid);
     p.L = m.num_layers;
     p.ht = y.ht;
-    // The bf16/fp16 planes run on k16 (ReLU masks in HBM, any depth) unless LNERF_K16=0 or the head
-    // is wider than one 16-wide tile; only the one-wave kernel keeps its masks in LDS, 1 KiB per
-    // hidden layer and wave in the bf16x6 budget: (L-1) <= kMaskTiles / 8. Past that depth the
-    // one-wave kernel falls back to exact f32 products.
-    const char* e = getenv("LNERF_K16");
-    const bool k16_wanted = !(e && e[0] == '0') && !(flags & LNERF_MFMA_F32) && m.n[p.L - 1] <= 16;
+    // The bf16/fp16 planes run on k16 (ReLU masks in HBM, any depth) unless the caller asks for the
+    // one-wave kernel pair (LNERF_ONE_WAVE, A/B runs) or the head is wider than one 16-wide tile;
+    // only the one-wave kernel keeps its masks in LDS, 1 KiB per hidden layer and wave in the
+    // bf16x6 budget: (L-1) <= kMaskTiles / 8. Past that depth it falls back to exact f32 products.
+    const bool k16_wanted = !(flags & LNERF_ONE_WAVE) && !(flags & LNERF_MFMA_F32) && m.n[p.L - 1] <= 16;
     const bool bf_ok = k16_wanted || (p.L - 1) <= kMaskTiles(true) / 8;
     p.x6 = (flags & LNERF_MFMA_F32) || !bf_ok ? 0
            : (flags & LNERF_MFMA_BF16)        ? 1
@@ -1699,12 +1691,14 @@ void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws
     p.mask_g = (unsigned long long*)(base + off);
     off += align_up(y.mask_total * 2, 64);
     p.wexp16 = (int*)(base + off);
-    p.smax16 = p.wexp16 + kMaxLayers;
+    p.dw_shift = p.wexp16 + kMaxLayers;
     off += 64;
     p.wmax_part = (int*)(base + off);
     off += align_up((size_t)kMaxLayers * kWmaxParts, 64);
-    p.smax_part = base + off;
-    if (train) off += align_up((size_t)2 * p.L * y.num_wg * 8, 64);
+    p.sexp = (signed char*)(base + off);
+    if (train) off += align_up((size_t)p.L * y.num_wg * 64, 64);   // L x num_wg x 128 x 2 bytes
+    p.epart = (int*)(base + off);
+    if (train) off += align_up((size_t)p.L * y.num_wg * 8, 64);
 
     p.x_off = y.x_off;
     p.ht16 = y.ht16;
@@ -1716,16 +1710,10 @@ void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws
         p.w16f_off[l] = y.w16f_off[l];
         p.w16b_off[l] = y.w16b_off[l];
     }
-    // LNERF_K16=0 selects the one-wave-per-SIMD kernel (fused_fwd_bwd_kernel) for A/B runs
-    // (k16_wanted implies k16_supported: x6 is 1 or 3 and the head fits one tile)
     p.k16 = k16_wanted && k16_supported(p) ? 1 : 0;
-    // fp16x3: kact (activations in LDS, 32x32 MFMA) with LNERF_KACT=1; k16 by default (kact is
-    // 1-3 % slower on cfg3)
-    const char* ek = getenv("LNERF_KACT");
-    p.kact = p.k16 && (ek && ek[0] == '1') && kact_supported(p) ? 1 : 0;
-    // dW: dw16_kernel for the bf16x6 split (LNERF_DW16=0: dw_all_kernel); one partial per split
-    const char* e2 = getenv("LNERF_DW16");
-    p.dw16 = (e2 && e2[0] == '0') ? 0 : (p.x6 == 3 || p.x6 == 2 ? 1 : 0);
+    // dW: dw16_kernel after k16 (it reads k16's slab layout and fp16x3 / bf16x6 planes); the
+    // one-wave kernel pairs with dw_all_kernel. One partial per split.
+    p.dw16 = p.k16;
     if (p.dw16)
         for (int l = 0; l < p.L; ++l) p.dw_phases[l] = 1;
 }
@@ -1859,13 +1847,10 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
         if (ev) (void)hipEventRecord(ev[i], s);
     };
     mark(0);
-    if (p.kact) kact_pack(p, ws, bs, s);
-    else if (p.k16) k16_pack(p, ws, bs, s);
+    if (p.k16) k16_pack(p, ws, bs, s);
     else launch_pack(p, ws, bs, s);
     mark(1);
-    if (p.kact) {
-        kact_launch(p, b, seed_loss ? 1.0f : seed, out, true, s);
-    } else if (p.k16) {
+    if (p.k16) {
         k16_launch(p, b, seed_loss ? 1.0f : seed, out, true, s);
     } else {
         FusedArgs fa = make_fused_args(p, b, seed_loss ? 1.0f : seed, out, true);
@@ -1935,10 +1920,7 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
 
 void fused_render(const FusedPlan& p, const float* ws, const float* bs, const lnerf_batch& b,
                   const lnerf_outputs& out, hipStream_t s) {
-    if (p.kact) {
-        kact_pack(p, ws, bs, s);
-        kact_launch(p, b, 1.0f, out, false, s);
-    } else if (p.k16) {
+    if (p.k16) {
         k16_pack(p, ws, bs, s);
         k16_launch(p, b, 1.0f, out, false, s);
     } else {

@@ -11,6 +11,20 @@ namespace lnerf {
 
 constexpr int kMaxLayers = LNERF_MAX_LAYERS;
 constexpr int kWmaxParts = 32;   // blocks per layer of the max|W| pass before the fp16x3 packing
+constexpr int kDefaultDwGrid = 512;   // dW workgroups per step unless LNERF_OPT_DW_GRID says otherwise
+
+// ---- fp16x3 exponent shifts ------------------------------------------------------------------
+// The shift e that puts a group's largest magnitude m in [2^13, 2^14) for the fp16 hi/lo split
+// (0 for m = 0 or non-finite m). Clamped to 2^127 so the scale 2^e stays a finite float even for
+// groups whose maximum is a tiny or subnormal value (m < 2^-113: underflowed transmittance, a
+// ray behind an opaque one); the unscale 2^-(e_w + e_x) is then still exact.
+__device__ __forceinline__ int fp16x3_shift(float m) {
+    if (!(m > 0.0f) || !(m < __builtin_inff())) return 0;
+    int e;
+    (void)__builtin_frexpf(m, &e);   // m = f 2^e, f in [0.5, 1)
+    const int sh = 14 - e;
+    return sh > 127 ? 127 : sh;
+}
 
 // ---- ray sampling (train_nerf.py:289-306), float64 as numpy computes it -----------------------
 // t_j = np.linspace(near, far, S)[j]: j * ((far - near) / (S - 1)) + near, the last one = far.
@@ -162,17 +176,18 @@ struct FusedPlan {
     int dw16;                            // 1: dW by dw16_kernel (lnerf_dw16.hip), one partial per split
     int* wexp16;                         // x6 = 2: per-layer max|W| bits (fp16 weight plane shifts)
     int* wmax_part;                      // x6 = 2: max|W| bits per layer and wmax block [L][kWmaxParts]
-    int* smax16;                         // x6 = 2: per-slab max bits ([l] input of layer l, [L+l] G_l)
-    float* smax_part;                    // x6 = 2: k1's per-wave slab maxima [2L][num_wg * 8]
-    int kact;                            // 1: k1 is kact_fwd_bwd_kernel (lnerf_kact.hip)
+    int* dw_shift;                       // dw16: per-layer product shift E_l (k1_reduce_kernel)
+    signed char* sexp;                   // dw16: k1's per-sample slab shifts [L][num_wg * 128][2]
+    int* epart;                          // dw16: k1's per-wave min of exA + exG [L][num_wg * 8]
 };
 
 bool fused_supported(const lnerf_mlp& mlp, int rays, int S, int input_mode, const char** why);
 // train = false sizes the forward-only (render) workspace: packed weights + loss partials.
-size_t fused_workspace_bytes(const lnerf_mlp& mlp, int rays, int S, bool train = true);
-// flags: LNERF_MFMA_F32 selects the exact f32 MFMA products over the default bf16x6 split
+// dw_grid: the dW kernel's workgroup budget (0 = kDefaultDwGrid; LNERF_OPT_DW_GRID).
+size_t fused_workspace_bytes(const lnerf_mlp& mlp, int rays, int S, bool train = true, int dw_grid = 0);
+// flags select the kernels and the MFMA precision (LNERF_MFMA_*, LNERF_ONE_WAVE; lnerf.h)
 void fused_plan(FusedPlan& p, const lnerf_mlp& mlp, const lnerf_batch& b, void* ws_base, int flags,
-                bool train = true);
+                bool train = true, int dw_grid = 0);
 // ev: nullable array of 7 events recorded between the step's kernels (LNERF_TIMING)
 void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, const lnerf_batch& b,
                       float seed, int flags, const lnerf_outputs& out, hipStream_t s,
@@ -183,15 +198,12 @@ void dw16_launch(const FusedPlan& p, hipStream_t s);
 // after a training k1: the batch loss (loss_total, out_loss) and, for dw16 with x6 = 2, the
 // layer-wide slab maxima, in one launch (lnerf_dw16.hip)
 void k1_reduce_launch(const FusedPlan& p, float* out_loss, hipStream_t s);
-// kact kernel entry points (lnerf_kact.hip): the fp16x3 k1 with the activations in LDS
-bool kact_supported(const FusedPlan& p);
-void kact_pack(const FusedPlan& p, const float* ws, const float* bs, hipStream_t s);
-void kact_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lnerf_outputs& out,
-                 bool want_grad, hipStream_t s);
 // k16 kernel entry points (lnerf_k16.hip)
 bool k16_supported(const FusedPlan& p);
 void k16_pack(const FusedPlan& p, const float* ws, const float* bs, hipStream_t s);
 void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lnerf_outputs& out,
                 bool want_grad, hipStream_t s);
+// the last training k1's ReLU decisions as (L-1, R, 32) bytes (lnerf_ctx_relu_masks)
+void k16_masks_launch(const FusedPlan& p, unsigned char* out, hipStream_t s);
 
 }  // namespace lnerf

@@ -38,30 +38,10 @@ typedef _Float16 hf8 __attribute__((ext_vector_type(8)));
 constexpr int kThreads = 512;
 constexpr int kWaves = 8;
 constexpr int kTile = comp::kTileSamples;     // 128 samples per workgroup
-constexpr int kMaxChunks = 2 * kMaxLayers * 8 + 2;   // <= 2 passes x 8 k-steps per layer + 2 end
+constexpr int kMaxChunks = 2 * kMaxLayers * 8 + 1;   // <= 2 passes x 8 k-steps per layer + 1 end
 constexpr int kMaxT = 16;                     // 16-feature tiles per 256-wide layer
-constexpr int kSlotBytes = kMaxT * 3 * 1024;  // one k-step of a 256-output layer, 3 planes
-// ring slot of a PL-plane kernel: one k-step of a 256-output layer
-template <int PL>
-constexpr int slot_bytes() { return kMaxT * PL * 1024; }
-// Staggered wave pairs (default): waves 0-3 ("early") meet the per-chunk barrier at the end of
-// a chunk, waves 4-7 ("late", each the SIMD partner of an early wave) in its middle, so the two
-// waves of a SIMD run their chunk prologues (DMA issue, slab stores, operand split, first
-// fragment reads) half a chunk apart, each under its partner's MFMAs. The ring then needs 3
-// slots: in one barrier period the late waves still read the previous chunk's second half while
-// every wave reads the current chunk and the next one lands (one chunk in flight; every wave
-// issues 1/8 of its pieces right after its own prologue).
-#ifndef LNERF_K16_STAGGER
-#define LNERF_K16_STAGGER 1
-#endif
-constexpr bool kStagger = LNERF_K16_STAGGER != 0;
-#ifndef LNERF_K16_AHEAD
-#define LNERF_K16_AHEAD 1
-#endif
-#ifndef LNERF_K16_LOADERS
-#define LNERF_K16_LOADERS 4
-#endif
-constexpr int kLoaders = kStagger ? 8 : LNERF_K16_LOADERS;   // waves that issue the weight DMA
+constexpr int kCompBytes = 2688 * 4;          // composite_tile's scratch (comp[0, 2688))
+constexpr int kLoaders = 8;                   // waves that issue the weight DMA (all)
 // timing experiments only (wrong results): drop the slab stores / the weight DMA after chunk 2
 #ifndef LNERF_K16_NOSTORE
 #define LNERF_K16_NOSTORE 0
@@ -69,17 +49,30 @@ constexpr int kLoaders = kStagger ? 8 : LNERF_K16_LOADERS;   // waves that issue
 #ifndef LNERF_K16_NODMA
 #define LNERF_K16_NODMA 0
 #endif
-// unstaggered: chunks in flight while one computes: 1 (a 2-slot ring) or 2 (a 3-slot ring;
-// measured slower)
-constexpr int kAhead = kStagger ? 1 : LNERF_K16_AHEAD;
-static_assert(kAhead == 1 || kAhead == 2, "the ring has room for two chunks in flight at most");
-constexpr int kSlots = kStagger ? 3 : kAhead + 1;   // ring slots
-constexpr int kOffComp = 3 * kSlotBytes;      // room for the deepest ring
-constexpr int kCompBytes = 2688 * 4;          // composite_tile's scratch (comp[0, 2688))
-constexpr int kOffRay = kOffComp + kCompBytes;
-constexpr int kOffBias = kOffRay + kTile * 4;
-constexpr int kLdsBytes = kOffBias + 3 * 256 * 4;   // + a 3-slot ring of layer biases
-static_assert(kLdsBytes + 1024 <= 160 * 1024, "LDS budget (+1 KiB for the profiling build)");
+
+// The weight stream of a PL-plane kernel. A chunk is KC k-steps (32 input features each) x every
+// output tile x PL planes, delivered by LDS-DMA into one slot of a ring, one workgroup barrier per
+// chunk (the barrier count, not the bytes, is what a 32-deep k-step costs: BK 64 over 32).
+//  * fp16x3 / plain bf16 (PL <= 2): KC = 2 (64 KiB per chunk at 16 tiles x 2 planes), two slots:
+//    chunk c + 1 lands while chunk c is computed.
+//  * bf16x6 (PL = 3): KC = 1 -- two 96 KiB chunks would not fit -- with staggered wave pairs:
+//    waves 0-3 meet the per-chunk barrier at the end of a chunk, waves 4-7 (each the SIMD partner
+//    of an early wave) in its middle, so the two waves of a SIMD run their chunk prologues half a
+//    chunk apart; the ring then needs 3 slots (the late waves still read the previous chunk
+//    while every wave reads the current one and the next one lands).
+template <int PL>
+struct Ring {
+    static constexpr int KC = PL == 3 ? 1 : 2;
+    static constexpr bool stagger = PL == 3;
+    static constexpr int slots = stagger ? 3 : 2;
+    static constexpr int slot_bytes = KC * kMaxT * PL * 1024;
+    static constexpr int off_comp = slots * slot_bytes;
+    static constexpr int off_ray = off_comp + kCompBytes;
+    static constexpr int off_bias = off_ray + kTile * 4;
+    static constexpr int lds_bytes = off_bias + 3 * 256 * 4;   // + a 3-slot ring of layer biases
+    static_assert(lds_bytes + 1024 <= 160 * 1024, "LDS budget (+1 KiB for the profiling build)");
+    static_assert((KC * kMaxT - 1) * PL * 1024 < 65536, "ds_read offsets are 16-bit immediates");
+};
 
 struct K16Args {
     int L;
@@ -113,8 +106,11 @@ struct K16Args {
     int want_grad;
     int planes;
     const int* wexp;   // PL = 2: per-layer max|W| bits of the packed fp16 weight planes (wshift_of)
-    float* smax;       // PL = 2, training: per-wave slab maxima [2L][num_wg * 8]: slab l the input
-                       // of layer l (X, A_l-1), slab L + l G_l
+    // training: every sample's exponent shift of each slab row (store_sexp), [l][position][2] int8:
+    // byte 0 the input of layer l (X, A_l-1), byte 1 G_l; position = half-block * 16 + sample
+    signed char* sexp;
+    int rpad;          // slab positions (num_wg * 128)
+    int* epart;        // training: per-wave min over samples of exA + exG, [l][num_wg * 8]
 };
 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
@@ -174,8 +170,6 @@ __device__ __forceinline__ int dma_chunk(const K16Args& a, const ChunkT& c, unsi
     const int tid = threadIdx.x, wave = wave_id();
     int n = 0;
     if (!c.src) return 0;
-    // loader waves 0..kLoaders-1 (waves w and w+4 share a SIMD: with 4 loaders each SIMD keeps
-    // one wave free of DMA issue to feed the matrix core)
     if (wave >= kLoaders) return 0;
     for (int off = wave * 1024; off < c.bytes; off += kLoaders * 1024) {
         const char* g = (const char*)c.src + off + (tid & 63) * 16;
@@ -207,12 +201,14 @@ __device__ __forceinline__ void vm_wait_n(int n, std::integer_sequence<int, N...
     n = n > 63 ? 63 : n;
     ((n == N ? vm_wait<N>() : void()), ...);
 }
-// pending < 0: this wave has no DMA piece to wait for (only the barrier)
+// pending < 0: this wave has no DMA piece to wait for (only the barrier); otherwise the number of
+// this wave's vector-memory operations issued after its pieces (the chunk's slab stores)
 __device__ __forceinline__ void dma_barrier(int pending) {
     PROF_T(t0);
     asm volatile("" ::: "memory");
     if (pending == 0) vm_wait<0>();
-    else if (pending == 8) vm_wait<8>();   // kAhead = 1: a loader wave behind its slab stores
+    else if (pending == 2) vm_wait<2>();
+    else if (pending == 4) vm_wait<4>();
     else if (pending > 0) vm_wait_n(pending, std::make_integer_sequence<int, 64>{});
     PROF_ADD(kPfVm, t0);
     __builtin_amdgcn_s_barrier();
@@ -237,15 +233,9 @@ __device__ __forceinline__ void split_h(float xs, _Float16& h, _Float16& l) {
     l = (_Float16)(xs - (float)h);
 }
 
-// the exponent shift ew of a layer from its max|W| bits: max|W| 2^ew in [2^13, 2^14) (0 for an
-// all-zero or non-finite layer) -- the weight-side half of the fp16x3 scaling
-__device__ __forceinline__ int wshift_of(int maxbits) {
-    const float mx = __int_as_float(maxbits);
-    if (!(mx > 0.0f) || !(mx < __builtin_inff())) return 0;
-    int e;
-    (void)__builtin_frexpf(mx, &e);
-    return 14 - e;
-}
+// the exponent shift ew of a layer from its max|W| bits (fp16x3_shift) -- the weight-side half
+// of the fp16x3 scaling
+__device__ __forceinline__ int wshift_of(int maxbits) { return fp16x3_shift(__int_as_float(maxbits)); }
 
 // The same split for a pair (x0, x1) packed as two f16 per register, with v_fma_mix: hi =
 // round_f16(x sc) and lo = round_f16(x sc - hi) are fused multiply-adds with one rounding to f16
@@ -268,16 +258,14 @@ __device__ __forceinline__ void split_x(float x, __bf16& h, __bf16& m, __bf16& l
     l = (__bf16)(r - (float)m);
 }
 
-// Slab tile store: the 8 features of k-step s that a lane holds (rows phi - 32 s of the
-// 32-feature tile) for its sample n, into [32 rows][16 samples] of this wave's half. Each wave
-// instruction writes 4 runs of 64 B.
+// Slab tile store: the 8 features of k-step s that a lane holds for its sample n (registers 0-3 of
+// tiles 2s and 2s+1 = features 4g ..+3 and 16 + 4g ..+3 of the 32-feature tile) into this wave's
+// sample-major half-block [feature half 2][16 samples][16 features]: two global_store_dwordx4,
+// each wave instruction one contiguous 1 KiB (lnerf_dw16.hip reads it back transposed).
 __device__ __forceinline__ void store_slab_step(float* __restrict__ dst, const fx4& t0, const fx4& t1) {
     const int lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const int row = 16 * (j >> 2) + 4 * g + (j & 3);
-        __builtin_nontemporal_store(j < 4 ? t0[j] : t1[j - 4], dst + row * 16 + n);
-    }
+    __builtin_nontemporal_store(t0, (fx4*)(dst + n * 16 + 4 * g));
+    __builtin_nontemporal_store(t1, (fx4*)(dst + 256 + n * 16 + 4 * g));
 }
 
 // LDS byte address of a pointer into __shared__ memory.
@@ -319,7 +307,7 @@ __device__ __forceinline__ void read_tile(unsigned base, bf8 (&w)[3]) {
 }
 
 // Output tile O of one k-step: issue the reads of tile O + kDist, wait for tile O's (leaving
-// the younger ones in flight), six MFMAs (small terms first).
+// the younger ones in flight), the MFMAs (small terms first).
 template <int NTO, int PL, int O>
 __device__ __forceinline__ void tile_step(unsigned base, bf8 (&w)[kDist + 1][3], const bf8& bh,
                                           const bf8& bm, const bf8& bl, fx4 (&out)[kMaxT]) {
@@ -373,12 +361,13 @@ __device__ __forceinline__ void make_b(const fx4 (&in)[kMaxT], int s, int ex, bf
         bh = __builtin_bit_cast(bf8, hv);
         bm = __builtin_bit_cast(bf8, lv);
     } else {
+        const float sc = PL == 3 ? __builtin_ldexpf(1.0f, ex) : 1.0f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const float x = j < 4 ? in[2 * s][j] : in[2 * s + 1][j - 4];
             if (PL == 3) {
                 __bf16 h, m, l;
-                split_x(x, h, m, l);
+                split_x(x * sc, h, m, l);
                 bh[j] = h;
                 bm[j] = m;
                 bl[j] = l;
@@ -392,61 +381,70 @@ __device__ __forceinline__ void make_b(const fx4 (&in)[kMaxT], int s, int ex, bf
     }
 }
 
-// One pass (a layer's forward or backward MMA): out[o] += sum over the pass's k-steps of
-// Wpack[s][o] (x) in[2s..2s+1], NTO output tiles. Chunk ci is read from ring slot ci % kSlots
-// while chunk ci+kAhead (issued here) lands. `slab` (nullable)
-// receives the input tiles (the A_{l-1} or G_l slab of this wave's half-block).
+// One k-step s of a pass (compile-time after unrolling): out[o] += Wpack[s][o] (x) in[2s..2s+1]
+// from sub-step kk of ring slot ci % slots. The chunk's first k-step (kk = 0) issues the DMA of
+// chunk ci + 1 and its last (LAST) meets the barrier that waits for it. (bh, bm, bl) hold k-step
+// s's B planes on entry and k-step s + 1's on exit. `slab` (nullable) receives the input tiles
+// (the A_{l-1} or G_l slab of this wave's half-block).
+template <int NTO, int PL>
+__device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk, bool last, int& ci,
+                                         unsigned char* ring, float* bias_ring, const fx4 (&in)[kMaxT],
+                                         fx4 (&out)[kMaxT], float* __restrict__ slab, int ex, bf8& bh,
+                                         bf8& bm, bf8& bl, int& pending) {
+    using R = Ring<PL>;
+    const int lane = threadIdx.x & 63;
+    const unsigned base = lds_addr(ring + (ci % R::slots) * R::slot_bytes) + kk * NTO * PL * 1024 + lane * 16;
+    const bool st = slab && !LNERF_K16_NOSTORE;
+    if (kk == 0) {
+        // DMA of chunk ci + 1 first (its table entry is a scalar load the compiler waits for
+        // with lgkmcnt(0), which would also wait for the fragment reads), then the first weight
+        // tiles, in flight while the slab stores and the operand split issue. The barrier waits
+        // for this wave's pieces of chunk ci + 1 only: the slab stores issued after them (two
+        // per k-step) stay in flight.
+        const int issued = (LNERF_K16_NODMA && ci >= 2)
+                               ? 0
+                               : dma_chunk(a, chunk_at(a, ci + 1),
+                                           ring + ((ci + 1) % R::slots) * R::slot_bytes, bias_ring);
+        asm volatile("" ::: "memory");   // the slab stores stay younger than the pieces
+        pending = issued ? 0 : -1;
+    }
+    if (st && pending >= 0) pending += 2;
+    const bool late = R::stagger && wave_id() >= 4;
+    bf8 w[kDist + 1][3];
+    read_tile<PL, 0>(base, w[0]);
+    if constexpr (NTO > 1) read_tile<PL, 1>(base, w[1]);
+    static_assert(kDist == 2, "the prologue reads kDist tiles");
+    if (st) store_slab_step(slab + s * 1024, in[2 * s], in[2 * s + 1]);
+    // first half of the output tiles, [late waves: barrier], the next k-step's operand split (off
+    // the next prologue's critical path), second half, [early: barrier]
+    constexpr int H = (NTO + 1) / 2;
+    tile_steps<NTO, PL, 0>(std::make_integer_sequence<int, H>{}, base, w, bh, bm, bl, out);
+    if (late && last) dma_barrier(pending);
+    bf8 nh = {}, nm = {}, nl = {};
+    if (s + 1 < ks) make_b<PL>(in, s + 1 < 8 ? s + 1 : 0, ex, nh, nm, nl);
+    tile_steps<NTO, PL, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, bh, bm, bl, out);
+    if (!late && last) dma_barrier(pending);
+    if (last) ++ci;
+    bh = nh;
+    bm = nm;
+    bl = nl;
+}
+
+// One pass (a layer's forward or backward MMA) over its ks k-steps, Ring::KC k-steps per chunk.
 template <int NTO, int PL>
 __device__ __forceinline__ void k16_pass(const K16Args& a, int ks, int& ci, unsigned char* ring,
                                          float* bias_ring, const fx4 (&in)[kMaxT], fx4 (&out)[kMaxT],
                                          float* __restrict__ slab, int ex = 0) {
-    const int lane = threadIdx.x & 63;
-    constexpr int kSB = slot_bytes<PL>();
+    constexpr int KC = Ring<PL>::KC;
     bf8 bh = {}, bm = {}, bl = {};
     make_b<PL>(in, 0, ex, bh, bm, bl);
+    int pending = 0;
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
         if (s < ks) {
-            const unsigned base = lds_addr(ring + (ci % kSlots) * kSB) + lane * 16;
-            // DMA of chunk ci+AHEAD first (its table entry is a scalar load the compiler waits for
-            // with lgkmcnt(0), which would also wait for the fragment reads), then the first
-            // weight tiles, in flight while the slab stores and the operand split issue
-            // The barrier waits for this wave's pieces of chunk ci+1 only: the vector-memory
-            // operations younger than them stay in flight -- this k-step's 8 slab stores and
-            // (kAhead = 2) chunk ci+2's pieces. A wave that issues no DMA does not wait at all
-            // (its slab stores need no completion before the barrier).
-            // (register staging -- 16-B loads after the prologue, ds_write_b128 before the barrier
-            // -- measured slower: 1.52 vs 1.40 ms)
-            const int issued = (LNERF_K16_NODMA && ci >= 2)
-                                   ? 0
-                                   : dma_chunk(a, chunk_at(a, ci + kAhead),
-                                               ring + ((ci + kAhead) % kSlots) * kSB, bias_ring);
-            asm volatile("" ::: "memory");   // the slab stores stay younger than the pieces
-            const int nst = (slab && !LNERF_K16_NOSTORE) ? 8 : 0;
-            const int pending = wave_id() >= kLoaders ? -1
-                                : kAhead == 1       ? (issued ? nst : -1)
-                                                    : issued + nst;
-            const bool late = kStagger && wave_id() >= 4;
-            bf8 w[kDist + 1][3];
-            read_tile<PL, 0>(base, w[0]);
-            if constexpr (NTO > 1) read_tile<PL, 1>(base, w[1]);
-            // (an LDS-transposed form -- 8 ds_write_b32 + 2 ds_read_b128 + 2 dwordx4 stores --
-            // measured slower: 2.13-2.18 vs 2.02-2.03 ms)
-            if (slab && !LNERF_K16_NOSTORE) store_slab_step(slab + s * 1024, in[2 * s], in[2 * s + 1]);
-            static_assert(kDist == 2, "the prologue reads kDist tiles");
-            // first half of the output tiles, [late waves: barrier], the next k-step's operand
-            // split (off the next prologue's critical path), second half, [early: barrier]
-            constexpr int H = (NTO + 1) / 2;
-            tile_steps<NTO, PL, 0>(std::make_integer_sequence<int, H>{}, base, w, bh, bm, bl, out);
-            if (late) dma_barrier(pending);
-            bf8 nh = {}, nm = {}, nl = {};
-            if (s + 1 < ks) make_b<PL>(in, s + 1 < 8 ? s + 1 : 0, ex, nh, nm, nl);
-            tile_steps<NTO, PL, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, bh, bm, bl, out);
-            if (!late) dma_barrier(pending);
-            bh = nh;
-            bm = nm;
-            bl = nl;
-            ++ci;
+            const int kk = s % KC;
+            const bool last = kk == KC - 1 || s + 1 == ks;
+            k16_step<NTO, PL>(a, ks, s, kk, last, ci, ring, bias_ring, in, out, slab, ex, bh, bm, bl, pending);
         }
     }
 }
@@ -462,11 +460,9 @@ __device__ __forceinline__ void k16_pass_n(const K16Args& a, int ks, int& ci, un
     else k16_pass<16, PL>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
 }
 
-// PL = 2: the per-sample max|x| of a pass's input (lanes n, n + 16, n + 32, n + 48 hold sample
-// n's features), the basis of its exponent shift.
-template <int PL>
+// The per-sample max|x| of a pass's input (lanes n, n + 16, n + 32, n + 48 hold sample n's
+// features), the basis of its exponent shift (PL >= 2) and of dw16's balancing (training).
 __device__ __forceinline__ float sample_max(const fx4 (&in)[kMaxT]) {
-    if constexpr (PL != 2) return 0.0f;
     float m = 0.0f;
 #pragma unroll
     for (int o = 0; o < kMaxT; ++o)
@@ -476,23 +472,51 @@ __device__ __forceinline__ float sample_max(const fx4 (&in)[kMaxT]) {
     return __builtin_fmaxf(m, __shfl_xor(m, 32));
 }
 
-// the exponent shift ex with m 2^ex in [2^13, 2^14); 0 for m = 0 (or non-finite)
-__device__ __forceinline__ int shift_of(float m) {
-    if (!(m > 0.0f) || !(m < __builtin_inff())) return 0;
-    int e;
-    (void)__builtin_frexpf(m, &e);   // m = f 2^e, f in [0.5, 1)
-    return 14 - e;
+// the exponent shift ex with m 2^ex in [2^13, 2^14) (fp16x3_shift)
+__device__ __forceinline__ int shift_of(float m) { return fp16x3_shift(m); }
+
+// Training: this sample's exponent shift of one slab row (the shift its split used, or -128 for an
+// all-zero row), one byte per sample for dw16's per-sample balancing of A and G (lnerf_dw16.hip).
+// Issued before the pass's first DMA, so it is older than every piece a dma_barrier waits for.
+// Returns the byte.
+__device__ __forceinline__ int store_sexp(const K16Args& a, int l, int which, float m) {
+    const int lane = threadIdx.x & 63;
+    const int x = m > 0.0f ? shift_of(m) : -128;
+    if (lane < 16) {
+        const int p = (blockIdx.x * kWaves + (threadIdx.x >> 6)) * 16 + lane;
+        a.sexp[((size_t)l * a.rpad + p) * 2 + which] = (signed char)x;
+    }
+    return x;
 }
 
-// PL = 2, training: the wave's max of a slab, one plain store per wave and slab into
-// smax_part[slab][global wave] (k1_reduce_kernel folds them into dw16's layer-wide exponent
-// shifts; an atomic per wave on 2L shared words measured 2.2x slower for the whole kernel).
-// Issued before the pass's first DMA, so it is older than every piece a dma_barrier waits for.
-__device__ __forceinline__ void slab_max(float* part, int slab, float m) {
+// The forward's A-row shifts, one byte per layer packed in 4 registers (layer l in byte l % 4 of
+// word l / 4), so the backward pass can pair them with the G-row shifts without a memory round
+// trip. Selects instead of a dynamically indexed register array.
+struct ExPack {
+    unsigned w[4] = {0u, 0u, 0u, 0u};
+    __device__ __forceinline__ void put(int l, int x) {
+        const int sh = 8 * (l & 3);
 #pragma unroll
-    for (int d = 1; d < 16; d <<= 1) m = __builtin_fmaxf(m, __shfl_xor(m, d));
+        for (int k = 0; k < 4; ++k)
+            if (k == (l >> 2)) w[k] = (w[k] & ~(0xFFu << sh)) | ((unsigned)(x & 0xFF) << sh);
+    }
+    __device__ __forceinline__ int get(int l) const {
+        unsigned v = w[0];
+#pragma unroll
+        for (int k = 1; k < 4; ++k) v = k == (l >> 2) ? w[k] : v;
+        return (int)(signed char)((v >> (8 * (l & 3))) & 0xFFu);
+    }
+};
+
+// Training, after layer l's G-row shift xg: the wave's min over its samples of xa + xg (rows
+// marked -128 excluded), one plain store per wave into epart[l][global wave]; k1_reduce_kernel
+// folds them into dw16's per-layer product shift E_l.
+__device__ __forceinline__ void store_emin(const K16Args& a, int l, int xa, int xg) {
+    int v = (xa == -128 || xg == -128) ? (1 << 20) : xa + xg;
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) v = min(v, __shfl_xor(v, d));
     if ((threadIdx.x & 63) == 0)
-        part[(size_t)slab * gridDim.x * kWaves + blockIdx.x * kWaves + (threadIdx.x >> 6)] = m;
+        a.epart[(size_t)l * gridDim.x * kWaves + blockIdx.x * kWaves + (threadIdx.x >> 6)] = v;
 }
 
 // The layer's biases in the accumulator layout (fx4 = 4 consecutive features of a lane group),
@@ -526,11 +550,12 @@ __device__ __forceinline__ void zero_tiles(fx4 (&t)[kMaxT]) {
 // 2 = fp16x3, both fp32-class; 1 = plain bf16, inference).
 template <int HT, int PL>
 __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
-    __shared__ __attribute__((aligned(16))) unsigned char lds[kLdsBytes];
+    using R = Ring<PL>;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[R::lds_bytes];
     unsigned char* ring = lds;
-    float* comp = (float*)(lds + kOffComp);
-    float* rayloss = (float*)(lds + kOffRay);
-    float* bias_ring = (float*)(lds + kOffBias);
+    float* comp = (float*)(lds + R::off_comp);
+    float* rayloss = (float*)(lds + R::off_ray);
+    float* bias_ring = (float*)(lds + R::off_bias);
 
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id(), g = lane >> 4, n = lane & 15;
     const int wg = blockIdx.x;
@@ -549,11 +574,14 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
 
     fx4 act[kMaxT], out[kMaxT];
     zero_tiles(act);
+    ExPack exa;   // training: the forward's A-row shift of this lane's sample, per layer
     // PL = 2: layer l's weight exponent shift in lane l (read with readlane per pass); a pass's
     // accumulators carry 2^(ex + ew), removed exactly (powers of two) in its epilogue
     const int wexp_lane = (PL == 2 && lane < a.L) ? wshift_of(a.wexp[lane]) : 0;
+    // PL = 3 (bf16x6): the activations carry the per-sample shift too (bf16 spans fp32's range,
+    // but the mid / lo planes of values below ~2^-110 would be subnormal); the weights do not
     auto unscale = [&](int l, int ex) -> int {
-        return PL == 2 ? -(ex + __builtin_amdgcn_readlane(wexp_lane, l)) : 0;
+        return PL == 2 ? -(ex + __builtin_amdgcn_readlane(wexp_lane, l)) : PL == 3 ? -ex : 0;
     };
 
     // ---- layer-0 input in the accumulator layout, through a per-wave LDS scratch (the ring is
@@ -604,7 +632,7 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
 
     int ci = 0;   // chunk stream position (chunk_at)
     dma_chunk(a, chunk_at(a, 0), ring, bias_ring);
-    dma_barrier(kAhead == 2 ? dma_chunk(a, chunk_at(a, 1), ring + slot_bytes<PL>(), bias_ring) : 0);
+    dma_barrier(0);
     PROF_ADD(kPfPE, t_start);
     // ReLU mask bits of this wave, per hidden layer: [L-1][lane] u64
     unsigned long long* mask_w = a.mask_g + ((size_t)wg * (a.L - 1) * kWaves + wave) * 64 + lane;
@@ -617,8 +645,8 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
                                 half * 512;
         zero_tiles(out);
         const unsigned bl = lds_addr(bias_ring + (l % 3) * 256) + g * 16;
-        const float xm = sample_max<PL>(act);
-        if (PL == 2 && st) slab_max(a.smax, l, xm);
+        const float xm = (PL >= 2 || st) ? sample_max(act) : 0.0f;
+        if (st) exa.put(l, store_sexp(a, l, 0, xm));
         const int ex = shift_of(xm);
         const int sh = unscale(l, ex);
         if (l < a.L - 1) {
@@ -635,7 +663,7 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
             for (int o = 0; o < HT; ++o) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const float v = (PL == 2 ? __builtin_ldexpf(out[o][i], sh) : out[o][i]) + bv[o][i];
+                    const float v = (PL >= 2 ? __builtin_ldexpf(out[o][i], sh) : out[o][i]) + bv[o][i];
                     const bool pos = v > 0.0f;
                     act[o][i] = pos ? v : 0.0f;
                     mb |= (pos ? 1ull : 0ull) << (4 * o + i);
@@ -652,7 +680,7 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
             if (g == 0) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    comp[ls * 4 + i] = (PL == 2 ? __builtin_ldexpf(out[0][i], sh) : out[0][i]) + bv[0][i];
+                    comp[ls * 4 + i] = (PL >= 2 ? __builtin_ldexpf(out[0][i], sh) : out[0][i]) + bv[0][i];
             }
         }
     }
@@ -682,8 +710,8 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
         float* slab = a.grad + a.grad_off[l] + blk * (size_t)(a.nt[l] * 1024) + half * 512;
         PROF_T(t_b);
         const unsigned long long mb = mask_w[(size_t)(l - 1) * kWaves * 64];   // in flight over the pass
-        const float xm = sample_max<PL>(act);
-        if (PL == 2) slab_max(a.smax, a.L + l, xm);
+        const float xm = sample_max(act);
+        store_emin(a, l, exa.get(l), store_sexp(a, l, 1, xm));
         const int ex = shift_of(xm);
         const int sh = unscale(l, ex);
         k16_pass<HT, PL>(a, a.ks_b[l], ci, ring, bias_ring, act, out, slab, ex);
@@ -693,7 +721,7 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
         for (int o = 0; o < HT; ++o)
 #pragma unroll
             for (int i = 0; i < 4; ++i)
-                act[o][i] = ((mb >> (4 * o + i)) & 1ull) ? (PL == 2 ? __builtin_ldexpf(out[o][i], sh) : out[o][i])
+                act[o][i] = ((mb >> (4 * o + i)) & 1ull) ? (PL >= 2 ? __builtin_ldexpf(out[o][i], sh) : out[o][i])
                                                          : 0.0f;
         PROF_ADD(kPfBwdEpi, t_be);
     }
@@ -703,8 +731,8 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
     if (a.d_x) {
         // d_layer_input = G_0 W_0^T (ENCODED mode); the pass also writes G_0's slab
         zero_tiles(out);
-        const float xm = sample_max<PL>(act);
-        if (PL == 2) slab_max(a.smax, a.L, xm);
+        const float xm = sample_max(act);
+        store_emin(a, 0, exa.get(0), store_sexp(a, 0, 1, xm));
         const int ex = shift_of(xm);
         const int sh = unscale(0, ex);
         k16_pass_n<PL>(a, a.ks_b[0], ci, ring, bias_ring, a.to_b[0], act, out, g0, ex);
@@ -715,12 +743,12 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         const int f = 16 * o + 4 * g + i;
-                        if (f < a.k0) a.d_x[(size_t)gs * a.k0 + f] = PL == 2 ? __builtin_ldexpf(out[o][i], sh) : out[o][i];
+                        if (f < a.k0) a.d_x[(size_t)gs * a.k0 + f] = PL >= 2 ? __builtin_ldexpf(out[o][i], sh) : out[o][i];
                     }
                 }
         }
     } else {
-        if (PL == 2) slab_max(a.smax, a.L, sample_max<PL>(act));
+        store_emin(a, 0, exa.get(0), store_sexp(a, 0, 1, sample_max(act)));
 #pragma unroll
         for (int s = 0; s < 8; ++s)
             if (s < a.ks_b[0]) store_slab_step(g0 + s * 1024, act[2 * s], act[2 * s + 1]);
@@ -822,7 +850,32 @@ __global__ void pack16_kernel(Pack16Args a) {
     }
 }
 
+// ReLU decisions of the last training k1 as a dense bitmap: out[(l R + r) 32 + f / 8] bit f % 8 =
+// feature f of hidden layer l at sample row r was positive (nerf.py:141-144). One thread per
+// output byte; the bits come from two lanes' u64 mask words (lane g 16 + n holds features
+// 16 o + 4 g + i in bits 4 o + i).
+__global__ void k16_masks_kernel(const unsigned long long* __restrict__ mask_g, int L1, int R, int tile_samples,
+                                 unsigned char* __restrict__ out) {
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (size_t)L1 * R * 32) return;
+    const int b = (int)(idx & 31);
+    const size_t lr = idx >> 5;
+    const int l = (int)(lr / R), r = (int)(lr % R);
+    const int wg = r / tile_samples, ls = r % tile_samples, wave = ls >> 4, n = ls & 15;
+    const int o = b >> 1, g0 = 2 * (b & 1);
+    const unsigned long long* w = mask_g + ((size_t)(wg * L1 + l) * kWaves + wave) * 64;
+    const unsigned lo = (unsigned)(w[g0 * 16 + n] >> (4 * o)) & 0xFu;
+    const unsigned hi = (unsigned)(w[(g0 + 1) * 16 + n] >> (4 * o)) & 0xFu;
+    out[idx] = (unsigned char)(lo | (hi << 4));
+}
+
 }  // namespace
+
+void k16_masks_launch(const FusedPlan& p, unsigned char* out, hipStream_t s) {
+    const size_t n = (size_t)(p.L - 1) * p.R * 32;
+    if (n == 0) return;
+    k16_masks_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(p.mask_g, p.L - 1, p.R, p.rays_per_wg * p.S, out);
+}
 
 bool k16_supported(const FusedPlan& p) {
     if (p.x6 != 3 && p.x6 != 2 && p.x6 != 1) return false;
@@ -904,24 +957,33 @@ void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lner
     a.want_grad = want_grad ? 1 : 0;
     a.planes = p.x6;
     a.wexp = p.wexp16;
-    a.smax = p.smax_part;
-    // the chunk stream: forward 0..L-1, backward L-1..1 (training), backward 0 (d_x)
+    a.sexp = p.sexp;
+    a.rpad = p.num_wg * 128;
+    a.epart = p.epart;
+    // the chunk stream: forward 0..L-1, backward L-1..1 (training), backward 0 (d_x); chunks of
+    // KC k-steps (Ring: 2 for fp16x3 / bf16, 1 for bf16x6), the pack layout's consecutive k-steps
     {
+        const int KC = p.x6 == 3 ? 1 : 2;
         int ci = 0;
         auto add = [&](bool fwd, int l) {
             const int ks = fwd ? a.ks_f[l] : a.ks_b[l], to = fwd ? a.to_f[l] : a.to_b[l];
-            const size_t per = (size_t)to * a.planes * 512;   // u16
-            for (int s2 = 0; s2 < ks; ++s2, ++ci) {
+            const size_t per = (size_t)to * a.planes * 512;   // u16 per k-step
+            for (int s2 = 0; s2 < ks; s2 += KC, ++ci) {
+                const int nk = ks - s2 < KC ? ks - s2 : KC;
                 a.chunk_tab[2 * ci] = (unsigned)((fwd ? a.wf_off[l] : a.wb_off[l]) + (size_t)s2 * per);
-                a.chunk_tab[2 * ci + 1] = (unsigned)(per * 2 / 1024) | ((fwd && s2 == 0 ? l + 1 : 0) << 16);
+                a.chunk_tab[2 * ci + 1] = (unsigned)(nk * per * 2 / 1024) | ((fwd && s2 == 0 ? l + 1 : 0) << 16);
             }
         };
         for (int l = 0; l < p.L; ++l) add(true, l);
         if (want_grad)
             for (int l = p.L - 1; l >= (a.d_x ? 0 : 1); --l) add(false, l);
-        // two zero entries past the end (the kernel looks two chunks ahead): a{} zeroed them
+        // a zero entry past the end (the kernel looks one chunk ahead): a{} zeroed it
     }
     static_assert(sizeof(K16Args) <= 4096, "kernel arguments");
+#ifdef LNERF_K16_ONLY_16_2   // compile-time experiments: one instantiation
+    k16_fwd_bwd_kernel<16, 2><<<p.num_wg, kThreads, 0, s>>>(a);
+    return;
+#endif
 #define LNERF_K16_LAUNCH(HT)                                                              \
     if (p.x6 == 3) k16_fwd_bwd_kernel<HT, 3><<<p.num_wg, kThreads, 0, s>>>(a);            \
     else if (p.x6 == 2) k16_fwd_bwd_kernel<HT, 2><<<p.num_wg, kThreads, 0, s>>>(a);       \

@@ -32,6 +32,9 @@ MFMA_F32 = 64     # fused path: exact f32 MFMA instead of the default fp16x3 spl
 MFMA_BF16 = 128   # fused path: plain bf16 operands (reduced precision; inference)
 MFMA_F16X3 = 256  # fused path: fp16x3 split (22-bit products, fp32 accumulate; the k16 default)
 MFMA_BF16X6 = 512  # fused path: bf16x6 split (fp32-accurate products)
+ONE_WAVE = 1024    # fused path: the one-wave-per-SIMD kernel pair instead of k16 + dw16 (A/B)
+
+OPT_DW_GRID = 1    # lnerf_ctx_set_option: dW workgroups per step (0 = default 512)
 
 # every symbol include/lnerf.h declares (tests check the library exports all of them)
 EXPORTED_SYMBOLS = [
@@ -39,6 +42,7 @@ EXPORTED_SYMBOLS = [
     "mult_a_b", "lnerf_last_error", "lnerf_version", "lnerf_ctx_create", "lnerf_ctx_destroy",
     "lnerf_workspace_bytes", "lnerf_train_step", "lnerf_render", "lnerf_scale_by_device_scalar",
     "lnerf_adam_update", "lnerf_ctx_timings", "lnerf_get_rays", "lnerf_ctx_last_path",
+    "lnerf_ctx_set_option", "lnerf_ctx_relu_masks",
 ]
 
 # lnerf_ctx_last_path bits
@@ -46,7 +50,6 @@ PATH_GENERIC = 1
 PATH_FUSED = 2
 PATH_K16 = 4
 PATH_DW16 = 8
-PATH_KACT = 16
 
 
 class LnerfMLP(ctypes.Structure):
@@ -150,9 +153,12 @@ def configure(lib: ctypes.CDLL) -> None:
                                       ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
     lib.lnerf_ctx_timings.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
     lib.lnerf_ctx_last_path.argtypes = [ctypes.c_void_p]
+    lib.lnerf_ctx_set_option.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    lib.lnerf_ctx_relu_masks.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
     lib.lnerf_get_rays.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(ctypes.c_double), ctypes.c_void_p, ctypes.c_void_p]
-    for name in ("lnerf_ctx_timings", "lnerf_ctx_last_path", "lnerf_ctx_create", "lnerf_train_step", "lnerf_render",
+    for name in ("lnerf_ctx_timings", "lnerf_ctx_last_path", "lnerf_ctx_set_option", "lnerf_ctx_relu_masks",
+                 "lnerf_ctx_create", "lnerf_train_step", "lnerf_render",
                  "lnerf_scale_by_device_scalar", "lnerf_adam_update", "lnerf_get_rays"):
         getattr(lib, name).restype = ctypes.c_int
 
@@ -308,8 +314,25 @@ class Engine:
         if v < 0:
             raise RuntimeError(f"lnerf_ctx_last_path: {last_error()}")
         return dict(generic=bool(v & PATH_GENERIC), fused=bool(v & PATH_FUSED),
-                    k16=bool(v & PATH_K16), kact=bool(v & PATH_KACT), dw16=bool(v & PATH_DW16),
-                    planes=(v >> 8) & 3)
+                    k16=bool(v & PATH_K16), dw16=bool(v & PATH_DW16), planes=(v >> 8) & 3)
+
+    def relu_masks(self, L: int, R: int):
+        """The last training step's hidden ReLU decisions (k16 path): numpy bool (L-1, R, 256),
+        [l, r, f] = feature f of hidden layer l at sample row r was positive."""
+        import numpy as np
+        torch = self.torch
+        out = torch.empty((L - 1) * R * 32, dtype=torch.uint8, device=f"cuda:{self.device}")
+        rc = self.lib.lnerf_ctx_relu_masks(self.ctx, ctypes.c_void_p(out.data_ptr()), out.numel(),
+                                           self._stream())
+        if rc != 0:
+            raise RuntimeError(f"lnerf_ctx_relu_masks: {last_error()}")
+        bits = out.cpu().numpy().reshape(L - 1, R, 32)
+        return np.unpackbits(bits, axis=2, bitorder="little").astype(bool)
+
+    def set_option(self, option: int, value: int):
+        """lnerf_ctx_set_option (OPT_DW_GRID: the dW kernel's workgroup budget, 0 = default)."""
+        if self.lib.lnerf_ctx_set_option(self.ctx, option, value) != 0:
+            raise RuntimeError(f"lnerf_ctx_set_option: {last_error()}")
 
     def scale_by_device_scalar(self, buf, scale):
         rc = self.lib.lnerf_scale_by_device_scalar(ctypes.c_void_p(buf.data_ptr()), buf.numel(),

@@ -194,19 +194,30 @@ def without_relu_ties(w: Workload, thresh: float = 5e-7) -> Workload:
 # --------------------------------------------------------------------------------------------
 
 
-def nerf_forward_backward(X, ws, bs, dists, target, S, seed=1.0):
+def nerf_forward_backward(X, ws, bs, dists, target, S, seed=1.0, masks=None):
     """scripts/nerf.py:1-304 forward and the exact derivative its rev_diff computes (SURVEY §8a
     "Backward the build implements"), in float64. Returns a dict with loss, acc_color (N,3),
-    dW/db per layer, dX, d_dists, d_target, and the per-sample rgba."""
+    dW/db per layer, dX, d_dists, d_target, and the per-sample rgba.
+
+    seed=None seeds the reverse pass with the loss itself (train_nerf.py:477). masks (optional):
+    per hidden layer l a bool (R, n_l) array of ReLU decisions to use instead of z > 0 in both
+    passes (nerf.py:141-144) -- the derivative at another implementation's decisions, for
+    comparing with it on rays whose pre-activations sit at |z| ~ 0 (ReLU ties). Also returns the
+    hidden pre-activations Z[l] and their term magnitudes T[l] = |A||W| + |b|."""
     X = np.asarray(X, np.float64)
     L = len(ws)
     A = [X]
     Z = []
+    Tm = []
     for l in range(L):
-        z = A[-1] @ np.asarray(ws[l], np.float64) + np.asarray(bs[l], np.float64)[None, :]
+        W64 = np.asarray(ws[l], np.float64)
+        b64 = np.asarray(bs[l], np.float64)
+        z = A[-1] @ W64 + b64[None, :]
         Z.append(z)
         if l < L - 1:
-            A.append(np.where(z > 0, z, 0.0))
+            Tm.append(np.abs(A[-1]) @ np.abs(W64) + np.abs(b64)[None, :])
+            m = (z > 0) if masks is None else np.asarray(masks[l], bool)
+            A.append(np.where(m, z, 0.0))
     zl = Z[-1]
     sig = 1.0 / (1.0 + np.exp(-zl[:, :3]))
     sigma = np.where(zl[:, 3] > 0, zl[:, 3], 0.0)
@@ -224,6 +235,8 @@ def nerf_forward_backward(X, ws, bs, dists, target, S, seed=1.0):
     C = (w[:, :, None] * rgb).sum(1)
     t = np.asarray(target, np.float64)
     loss = ((C - t) ** 2).sum()
+    if seed is None:
+        seed = loss
 
     gC = 2.0 * seed * (C - t)
     gw = (gC[:, None, :] * rgb).sum(2)
@@ -251,8 +264,41 @@ def nerf_forward_backward(X, ws, bs, dists, target, S, seed=1.0):
         db[l] = g.sum(0)
         ga = g @ np.asarray(ws[l], np.float64).T
         if l > 0:
-            g = np.where(Z[l - 1] > 0, ga, 0.0)
+            m = (Z[l - 1] > 0) if masks is None else np.asarray(masks[l - 1], bool)
+            g = np.where(m, ga, 0.0)
         else:
             dX = ga
     return dict(loss=loss, acc=C, dW=dW, db=db, dX=dX, d_dists=gdist, d_target=-gC,
-                rgb=rgb, sigma=sg, weights=w, alpha=alpha)
+                rgb=rgb, sigma=sg, weights=w, alpha=alpha, Z=Z[:-1], T=Tm)
+
+
+def nerf_forward_backward_chunked(X, ws, bs, dists, target, S, seed, masks=None, rays_per_chunk=256):
+    """nerf_forward_backward over ray chunks (bounded memory at the full bench size), summing the
+    batch quantities. `seed` must be a number here (the gradient is linear in it); returns loss,
+    acc, dW, db, d_dists, d_target and, per hidden layer, the decisions that differ from z > 0
+    with their margins |z| / T (flip_margins)."""
+    X = np.asarray(X)
+    N = X.shape[0] // S
+    L = len(ws)
+    out = dict(loss=0.0, acc=[], dW=[0.0] * L, db=[0.0] * L, d_dists=[], d_target=[],
+               flip_margins=[[] for _ in range(L - 1)])
+    for lo in range(0, N, rays_per_chunk):
+        hi = min(N, lo + rays_per_chunk)
+        rows = slice(lo * S, hi * S)
+        ms = None if masks is None else [np.asarray(m[rows], bool) for m in masks]
+        r = nerf_forward_backward(X[rows], ws, bs, dists[lo:hi], target[lo:hi], S, seed=seed, masks=ms)
+        out["loss"] += r["loss"]
+        out["acc"].append(r["acc"])
+        out["d_dists"].append(r["d_dists"])
+        out["d_target"].append(r["d_target"])
+        for l in range(L):
+            out["dW"][l] = out["dW"][l] + r["dW"][l]
+            out["db"][l] = out["db"][l] + r["db"][l]
+        if ms is not None:
+            for l in range(L - 1):
+                flip = (r["Z"][l] > 0) != ms[l]
+                out["flip_margins"][l].append(np.abs(r["Z"][l][flip]) / np.maximum(r["T"][l][flip], 1e-300))
+    for k in ("acc", "d_dists", "d_target"):
+        out[k] = np.concatenate(out[k])
+    out["flip_margins"] = [np.concatenate(f) if f else np.zeros(0) for f in out["flip_margins"]]
+    return out

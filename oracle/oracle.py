@@ -159,7 +159,7 @@ def standard_forward_backward(X, wp, bp, shapes, dists, target, S, seed=None, dX
         adj.pop("X")
     nerf_grad(d, prim, adj, loss if seed is None else seed)
     return dict(loss=loss, acc=acc, dW=adj["W"], dB=adj["B"], dX=adj.get("X"),
-                d_dists=adj["dists"], d_target=adj["T"], d_io=adj["IO"], rgba=rgba)
+                d_dists=adj["dists"], d_target=adj["T"], d_io=adj["IO"], rgba=rgba, io=IO)
 
 
 def train_step(X, wp, bp, shapes, dists, target, S, threads=1):

@@ -1,0 +1,134 @@
+"""Parity of the fused (k16 + dw16) path on EVERY ray, ReLU ties included.
+
+A hidden pre-activation z within a few fp32 ulp of 0 is decided by summation order: the fused
+kernels (MFMA k-order, fp16x3 / bf16x6 splits) and the loma-order fp32 oracle may take different
+ReLU branches there, and a different branch moves that sample's whole gradient row (SURVEY.md
+§8c: "ReLU-mask flips ... reported separately"). Instead of dropping such rays, the check reads
+the decisions the GPU actually took (lnerf_ctx_relu_masks) and:
+
+ 1. compares every output on ALL rays with the float64 restatement (oracle/nerf_np.py,
+    scripts/nerf.py:1-306) evaluated at the GPU's decisions, within TOL64;
+ 2. asserts every decision that differs from float64's own z > 0 is a genuine tie
+    (|z| <= FLIP_MARGIN * sum|terms|) and reports how many there were;
+ 3. compares with the loma-order fp32 C oracle (nerf_oracle.c) on the rays whose decisions agree
+    with the oracle's own (its intermediate_outputs, nerf.py:141-144), re-running the GPU on that
+    subset when any ray differs, and reports how many rays were set aside.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+import nerf_np
+from loma_calls import assert_close
+
+# fp32-class fused precisions against float64 (measured: dW within 5e-7 of max|dW|)
+TOL64 = dict(rtol=1e-5, atol_scale=1e-5)
+# against the loma-order fp32 oracle (itself 1.2e-6 from float64)
+TOLC = dict(rtol=1e-5, atol_scale=1e-5)
+# a decision the GPU takes differently from float64 must be a tie at fp32 resolution
+FLIP_MARGIN = 2e-6
+
+LAST = {}   # stats of the last check (tests print / assert on them)
+
+
+def padded(per_layer, shape):
+    out = np.zeros(shape, np.float64)
+    for l, a in enumerate(per_layer):
+        a = np.asarray(a, np.float64)
+        if a.ndim == 2:
+            out[l, :a.shape[0], :a.shape[1]] = a
+        else:
+            out[l, :a.shape[0]] = a
+    return out
+
+
+def encoded_input(w, points):
+    import oracle
+    if points:
+        return oracle.positional_encoding_3d(w.pts32.astype(np.float64), w.F)
+    return np.ascontiguousarray(w.X, np.float32)
+
+
+def _dev(engine, a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(f"cuda:{engine.device}")
+
+
+def run_fused(engine, w, *, points=True, seed=None, flags=0, want_dx=False):
+    """One GPU training step on workload w; returns its outputs and its ReLU decisions."""
+    import lnerf
+    import torch
+    shapes = [x.shape for x in w.ws]
+    mlp = lnerf.make_mlp(shapes, w.wp.shape[1], w.wp.shape[2])
+    x = _dev(engine, w.pts32.reshape(-1, 3) if points else w.X)
+    r = engine.train_step(mlp, _dev(engine, w.wp), _dev(engine, w.bp), x, _dev(engine, w.dists),
+                          _dev(engine, w.target), samples=w.S,
+                          input_mode=lnerf.INPUT_POINTS if points else lnerf.INPUT_ENCODED,
+                          num_freqs=w.F, seed=seed, flags=lnerf.FAST | flags, want_per_ray=True,
+                          want_dx=want_dx)
+    torch.cuda.synchronize()
+    out = dict(loss=float(r.loss.item()), acc=r.acc_color.cpu().numpy(), dW=r.d_ws.cpu().numpy(),
+               dB=r.d_bs.cpu().numpy(), d_dists=r.d_dists.cpu().numpy(),
+               d_target=r.d_target.cpu().numpy())
+    if want_dx:
+        out["dX"] = r.d_x.cpu().numpy()
+    L = len(shapes)
+    path = engine.last_path()
+    assert path["k16"], path
+    m = engine.relu_masks(L, w.N * w.S)
+    out["masks"] = [m[l, :, :shapes[l][1]] for l in range(L - 1)]
+    return out
+
+
+def check_fused(engine, w, *, points=True, seed=None, flags=0, want_dx=False, tol64=TOL64,
+                tolc=TOLC, c_oracle=True):
+    import oracle
+    got = run_fused(engine, w, points=points, seed=seed, flags=flags, want_dx=want_dx)
+    X = encoded_input(w, points)
+    shapes = [x.shape for x in w.ws]
+    # 1. float64 at the GPU's decisions, every ray
+    ref = nerf_np.nerf_forward_backward(X, w.ws, w.bs, w.dists, w.target, w.S, seed=seed,
+                                        masks=got["masks"])
+    assert abs(got["loss"] - ref["loss"]) <= 1e-6 * abs(ref["loss"]), (got["loss"], ref["loss"])
+    assert_close("acc", got["acc"], ref["acc"], **tol64)
+    assert_close("dW", got["dW"], padded(ref["dW"], w.wp.shape), **tol64)
+    assert_close("dB", got["dB"], padded(ref["db"], w.bp.shape), **tol64)
+    assert_close("d_dists", got["d_dists"], ref["d_dists"], **tol64)
+    assert_close("d_target", got["d_target"], ref["d_target"], **tol64)
+    if want_dx:
+        assert_close("dX", got["dX"], ref["dX"], **tol64)
+    # 2. decisions that differ from float64's own are ties
+    flips, worst = 0, 0.0
+    for l in range(len(shapes) - 1):
+        f = (ref["Z"][l] > 0) != got["masks"][l]
+        if f.any():
+            mg = np.abs(ref["Z"][l][f]) / np.maximum(ref["T"][l][f], 1e-300)
+            flips += int(f.sum())
+            worst = max(worst, float(mg.max()))
+    assert worst <= FLIP_MARGIN, f"a ReLU decision differs from float64 at |z|/T = {worst:.3g}"
+    stats = dict(rays=w.N, flips_vs_f64=flips, worst_flip_margin=worst)
+    # 3. the loma-order fp32 oracle on the rays whose decisions agree with its own
+    if c_oracle:
+        want = oracle.standard_forward_backward(X, w.wp, w.bp, shapes, w.dists, w.target, w.S,
+                                                seed=seed, dX=want_dx)
+        R = w.N * w.S
+        bad = np.zeros(R, bool)
+        for l in range(len(shapes) - 1):
+            bad |= ((want["io"][l, :R, :shapes[l][1]] > 0) != got["masks"][l]).any(axis=1)
+        rays_bad = np.unique(np.nonzero(bad)[0] // w.S)
+        stats["rays_vs_c_oracle_set_aside"] = int(len(rays_bad))
+        g2 = got
+        if len(rays_bad):
+            keep = [r for r in range(w.N) if r not in set(rays_bad.tolist())]
+            sub = nerf_np.subset_rays(w, keep)
+            g2 = run_fused(engine, sub, points=points, seed=seed, flags=flags, want_dx=want_dx)
+            Xs = encoded_input(sub, points)
+            want = oracle.standard_forward_backward(Xs, sub.wp, sub.bp, shapes, sub.dists, sub.target,
+                                                    sub.S, seed=seed, dX=want_dx)
+        assert abs(g2["loss"] - want["loss"]) <= 1e-5 * abs(want["loss"]), (g2["loss"], want["loss"])
+        for k in ("acc", "dW", "dB", "d_dists", "d_target") + (("dX",) if want_dx else ()):
+            assert_close(k, g2[k], want[k], **tolc)
+    LAST.clear()
+    LAST.update(stats)
+    print("fused parity:", stats)
+    return got, stats

@@ -1,23 +1,27 @@
-"""GPU parity of the native batched path (fused MFMA kernels) against the C oracle, plus
-size-independent properties at the full bench size (4096 rays x 64 samples, 8x256 MLP).
+"""GPU parity of the native batched path (fused MFMA kernels) against the float64 restatement and
+the C oracle, plus size-independent properties at the full bench size (4096 rays x 64 samples,
+8x256 MLP).
 
-Tolerance (fp32, north_star "within 1e-4"): |got - want| <= 1e-4 |want| + 1e-4 max|want| per
-tensor. The fused path sums in a different order than the scalar loma-order oracle (MFMA k-order,
-split-K over samples), so it is not bit-exact; sample/ray indexing is exact by construction
-(tested with per-ray outputs). Every fused precision is checked: the default fp16x3 split
-(22-bit products on the fp16 MFMA with per-sample / per-layer exponent shifts), the bf16x6 split
-(fp32-accurate products on the bf16 MFMA, LNERF_MFMA_BF16X6) and the exact f32 MFMA
-(LNERF_MFMA_F32).
+The default path (k16 + dw16, fp16x3 split) and its bf16x6 variant are checked on EVERY ray with
+tests/fused_parity.py: float64 at the GPU's own ReLU decisions within 1e-5 (abs + max-scaled),
+every decision that differs from float64's a tie at fp32 resolution, and the loma-order fp32
+oracle on the rays whose decisions agree with its own. The one-wave kernel pair (exact f32 MFMA,
+LNERF_ONE_WAVE) keeps its masks in LDS, so its tests compare with the C oracle on the rays that
+hold no decision below fp32 resolution (nerf_np.without_relu_ties).
+
+Tolerance forms: |got - want| <= rtol |want| + atol_scale max|want| per tensor (loma_calls.py).
 """
 import numpy as np
 import pytest
 
 import nerf_np
+from fused_parity import TOL64, check_fused
 from loma_calls import assert_close
 
 pytestmark = pytest.mark.gpu
 
-TOL = dict(rtol=1e-4, atol_scale=1e-4)
+TOL = dict(rtol=1e-4, atol_scale=1e-4)       # north_star's 1e-4 (one-wave paths, vs C oracle)
+TOL_F32 = dict(rtol=1e-5, atol_scale=1e-5)   # exact f32 MFMA vs the C oracle
 
 
 def _dev(engine, a):
@@ -62,121 +66,141 @@ def compare(got, want, keys=("dW", "dB", "d_dists", "d_target"), tol=TOL):
         assert_close(k, got[k], want[k], **tol)
 
 
-PRECISIONS = [0, 64, 512]   # default (fp16x3 split), lnerf.MFMA_F32, lnerf.MFMA_BF16X6
+FUSED = [0, 512]      # k16 + dw16: default fp16x3 split, lnerf.MFMA_BF16X6
+ONE_WAVE = [64, 1024]  # one-wave pair: lnerf.MFMA_F32 (exact f32), lnerf.ONE_WAVE (bf16x6)
 
 
-@pytest.mark.parametrize("prec", PRECISIONS)
+def _one_wave_tol(prec):
+    return TOL_F32 if prec == 64 else TOL
+
+
+@pytest.mark.parametrize("prec", FUSED)
 @pytest.mark.parametrize("points", [True, False])
-def test_fused_cfg2_matches_oracle(engine, points, prec):
+def test_fused_cfg2_all_rays(engine, points, prec):
     """Config 2 (train_nerf-sized MLP 33->30->30->4), 1024 rays x 32 samples, seed = loss."""
-    w = nerf_np.without_relu_ties(nerf_np.make_workload("cfg2"))
-    got = run_native(engine, w, points=points, flags=prec)
-    want = oracle_ref(w, points=points)
-    compare(got, want)
+    check_fused(engine, nerf_np.make_workload("cfg2"), points=points, flags=prec)
 
 
-@pytest.mark.parametrize("prec", PRECISIONS)
-def test_fused_cfg3_subset_matches_oracle(engine, prec):
-    """The bench MLP (33->256x7->4) on 24 rays x 64 samples, seed = loss."""
-    w = nerf_np.without_relu_ties(nerf_np.make_workload("cfg3", rays=24))
+@pytest.mark.parametrize("prec", FUSED)
+def test_fused_cfg3_subset_all_rays(engine, prec):
+    """The bench MLP (33->256x7->4) on 48 rays x 64 samples, seed = loss."""
+    check_fused(engine, nerf_np.make_workload("cfg3", rays=48), flags=prec)
+
+
+@pytest.mark.parametrize("prec", ONE_WAVE)
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3"])
+def test_one_wave_matches_oracle(engine, cfg, prec):
+    w = nerf_np.without_relu_ties(nerf_np.make_workload(cfg, rays=24 if cfg == "cfg3" else None))
     got = run_native(engine, w, flags=prec)
-    want = oracle_ref(w)
-    compare(got, want)
+    path = engine.last_path()
+    assert path["fused"] and not path["k16"] and not path["dw16"], path
+    compare(got, oracle_ref(w), tol=_one_wave_tol(prec))
 
 
-@pytest.mark.parametrize("prec", PRECISIONS)
-def test_fused_nonuniform_widths(engine, prec):
-    """Hidden widths that differ per layer (33->128->256->64->100->4): every layer's MMA runs
-    with the widest layer's tile count over zero-padded packed weights."""
-    w = nerf_np.make_workload("cfg2", rays=40, samples=48)
+def _nonuniform(w):
     rng = np.random.RandomState(3)
     dims = [33, 128, 256, 64, 100, 4]
     ws = [(rng.randn(k, n) * np.sqrt(2.0 / k)).astype(np.float32) for k, n in zip(dims, dims[1:])]
     bs = [(rng.randn(n) * 0.5).astype(np.float32) for n in dims[1:]]
-    wp = np.zeros((len(ws), 256, 256), np.float32)
-    bp = np.zeros((len(ws), 256), np.float32)
-    for l, (a, b) in enumerate(zip(ws, bs)):
-        wp[l, :a.shape[0], :a.shape[1]] = a
-        bp[l, :b.shape[0]] = b
-    w = nerf_np.Workload(w.pts, w.pts32, w.X, w.dists, w.target, ws, bs, wp, bp, w.F, w.S, w.N)
-    w = nerf_np.without_relu_ties(w)
-    got = run_native(engine, w, flags=prec)
-    want = oracle_ref(w)
-    compare(got, want)
+    wp, bp = nerf_np.pad_weights(ws, bs)
+    wp2 = np.zeros((len(ws), 256, 256), np.float32)
+    bp2 = np.zeros((len(ws), 256), np.float32)
+    wp2[:, :wp.shape[1], :wp.shape[2]] = wp
+    bp2[:, :bp.shape[1]] = bp
+    return nerf_np.Workload(w.pts, w.pts32, w.X, w.dists, w.target, ws, bs, wp2, bp2, w.F, w.S, w.N)
 
 
-@pytest.mark.parametrize("prec", PRECISIONS + [128])
-def test_fused_deep_mlp(engine, prec):
-    """12 layers (33->64x11->4): the k16 kernel's chunk stream (2 passes x 11 hidden layers) and
-    its HBM ReLU masks beyond the 8 hidden layers the one-wave kernel keeps in LDS. The bf16
-    precisions must run on k16 (+ dw16 for bf16x6); MFMA_F32 on the one-wave kernel."""
-    import lnerf
-    w = nerf_np.make_workload("cfg2", rays=32, samples=32)
+@pytest.mark.parametrize("prec", FUSED)
+def test_fused_nonuniform_widths(engine, prec):
+    """Hidden widths that differ per layer (33->128->256->64->100->4): every layer's MMA runs
+    with the widest layer's tile count over zero-padded packed weights."""
+    check_fused(engine, _nonuniform(nerf_np.make_workload("cfg2", rays=40, samples=48)), flags=prec)
+
+
+def _deep(w):
     rng = np.random.RandomState(7)
     dims = [33] + [64] * 11 + [4]
     ws = [(rng.randn(k, n) * np.sqrt(2.0 / k)).astype(np.float32) for k, n in zip(dims, dims[1:])]
     bs = [(rng.randn(n) * 0.5).astype(np.float32) for n in dims[1:]]
-    wp = np.zeros((len(ws), 64, 64), np.float32)
-    bp = np.zeros((len(ws), 64), np.float32)
-    for l, (a, b) in enumerate(zip(ws, bs)):
-        wp[l, :a.shape[0], :a.shape[1]] = a
-        bp[l, :b.shape[0]] = b
-    w = nerf_np.Workload(w.pts, w.pts32, w.X, w.dists, w.target, ws, bs, wp, bp, w.F, w.S, w.N)
-    w = nerf_np.without_relu_ties(w)
-    got = run_native(engine, w, flags=lnerf.FAST | prec)
+    wp, bp = nerf_np.pad_weights(ws, bs)
+    return nerf_np.Workload(w.pts, w.pts32, w.X, w.dists, w.target, ws, bs, wp, bp, w.F, w.S, w.N)
+
+
+@pytest.mark.parametrize("prec", FUSED + ONE_WAVE + [128])
+def test_fused_deep_mlp(engine, prec):
+    """12 layers (33->64x11->4): the k16 kernel's chunk stream (2 passes x 11 hidden layers) and
+    its HBM ReLU masks beyond the 8 hidden layers the one-wave kernel keeps in LDS. The bf16
+    precisions run on k16 (+ dw16 for the splits); MFMA_F32 on the one-wave kernel, which falls
+    back to exact f32 past its mask budget (LNERF_ONE_WAVE too)."""
+    import lnerf
+    w = _deep(nerf_np.make_workload("cfg2", rays=32, samples=32))
+    if prec in FUSED:
+        check_fused(engine, w, flags=prec)
+        assert engine.last_path() == dict(generic=False, fused=True, k16=True, dw16=True,
+                                          planes={0: 2, 512: 3}[prec])
+        return
+    got = run_native(engine, nerf_np.without_relu_ties(w) if prec != 128 else w,
+                     flags=lnerf.FAST | prec)
     path = engine.last_path()
-    want_planes = {0: 2, 64: 0, 128: 1, 512: 3}[prec]
-    assert path["fused"] and path["planes"] == want_planes, path
-    # every bf16 / fp16 precision on k16 by default; fp16x3 on kact with LNERF_KACT=1
-    import os
-    want_kact = prec == 0 and os.environ.get("LNERF_KACT") == "1"
-    assert path["kact"] == want_kact and path["k16"] == (prec != 64 and not want_kact), path
-    assert path["dw16"] == (prec in (0, 512)), path
-    want = oracle_ref(w)
     if prec == 128:
         # plain bf16 operands (8 significant bits): a loose sanity bound, not the fp32 tolerance
+        assert path == dict(generic=False, fused=True, k16=True, dw16=True, planes=1), path
+        want = oracle_ref(w)
         assert abs(got["loss"] - want["loss"]) <= 2e-2 * abs(want["loss"]), (got["loss"], want["loss"])
         assert_close("dW", got["dW"], want["dW"], rtol=0.0, atol_scale=5e-2)
     else:
-        compare(got, want)
+        assert path == dict(generic=False, fused=True, k16=False, dw16=False, planes=0), path
+        compare(got, oracle_ref(nerf_np.without_relu_ties(w)), tol=TOL_F32)
 
 
 def test_default_path_is_k16_dw16(engine):
-    """The bench configuration (cfg3 MLP) runs k16 + dw16 with the fp16x3 split by default, kact
-    with LNERF_KACT=1, and the one-wave kernel with the bf16x6 split without k16."""
-    import os
+    """The bench configuration (cfg3 MLP) runs k16 + dw16 with the fp16x3 split by default, the
+    one-wave pair with bf16x6 under LNERF_ONE_WAVE; conflicting precision flags and an fp16x3
+    request the k16 kernel cannot serve are errors."""
+    import lnerf
     w = nerf_np.make_workload("cfg3", rays=8)
     run_native(engine, w, per_ray=False)
-    assert engine.last_path() == dict(generic=False, fused=True, k16=True, kact=False, dw16=True, planes=2)
-    os.environ["LNERF_KACT"] = "1"
+    assert engine.last_path() == dict(generic=False, fused=True, k16=True, dw16=True, planes=2)
+    run_native(engine, w, per_ray=False, flags=lnerf.MFMA_F16X3)
+    assert engine.last_path()["planes"] == 2
+    run_native(engine, w, per_ray=False, flags=lnerf.ONE_WAVE)
+    assert engine.last_path() == dict(generic=False, fused=True, k16=False, dw16=False, planes=3)
+    for bad in (lnerf.ONE_WAVE | lnerf.MFMA_F16X3, lnerf.MFMA_F16X3 | lnerf.MFMA_BF16X6,
+                lnerf.MFMA_BF16 | lnerf.MFMA_BF16X6):
+        with pytest.raises(RuntimeError):
+            run_native(engine, w, per_ray=False, flags=bad)
+    # the relu mask readout exists only after a k16 training step
+    with pytest.raises(RuntimeError):
+        engine.relu_masks(8, 8 * 64)
+
+
+def test_dw_grid_option(engine):
+    """LNERF_OPT_DW_GRID changes only the dW split (deterministic per setting, same result within
+    fp32 summation-order error); out-of-range values are rejected."""
+    import lnerf
+    w = nerf_np.make_workload("cfg3", rays=64)
+    a = run_native(engine, w, seed=1.0, per_ray=False)
+    engine.set_option(lnerf.OPT_DW_GRID, 64)
     try:
-        run_native(engine, w, per_ray=False)
-        assert engine.last_path() == dict(generic=False, fused=True, k16=False, kact=True, dw16=True, planes=2)
+        b = run_native(engine, w, seed=1.0, per_ray=False)
     finally:
-        del os.environ["LNERF_KACT"]
-    os.environ["LNERF_K16"] = "0"
-    try:
-        run_native(engine, w, per_ray=False)
-        assert engine.last_path() == dict(generic=False, fused=True, k16=False, kact=False, dw16=True, planes=3)
-    finally:
-        del os.environ["LNERF_K16"]
+        engine.set_option(lnerf.OPT_DW_GRID, 0)
+    assert_close("dW", b["dW"], a["dW"], rtol=1e-6, atol_scale=1e-6)
+    with pytest.raises(RuntimeError):
+        engine.set_option(lnerf.OPT_DW_GRID, 5)
+    with pytest.raises(RuntimeError):
+        engine.set_option(99, 1)
 
 
 def test_fused_ragged_rays_and_samples(engine):
     """S that does not divide the 128-sample tile (30, as train_nerf.py uses), a ray count that
     leaves a partial workgroup, and S = 1 / S = 128 edges."""
     for rays, S in ((37, 30), (5, 128), (300, 1), (3, 100)):
-        w = nerf_np.without_relu_ties(nerf_np.make_workload("cfg2", rays=rays, samples=S))
-        got = run_native(engine, w)
-        want = oracle_ref(w)
-        compare(got, want)
+        check_fused(engine, nerf_np.make_workload("cfg2", rays=rays, samples=S))
 
 
 def test_fused_dx_encoded(engine):
-    w = nerf_np.without_relu_ties(nerf_np.make_workload("cfg2", rays=64))
-    got = run_native(engine, w, points=False, seed=1.0, want_dx=True)
-    want = oracle_ref(w, points=False, seed=1.0, dX=True)
-    compare(got, want, keys=("dW", "dB", "dX"))
+    check_fused(engine, nerf_np.make_workload("cfg2", rays=64), points=False, seed=1.0, want_dx=True)
 
 
 def test_generic_native_matches_oracle(engine):
@@ -246,6 +270,38 @@ def test_full_size_fused_vs_generic(engine, full_noties):
     compare(a, b)
 
 
+def test_full_size_all_rays_float64(engine, full):
+    """The whole bench batch (262 144 samples, every ray) against the float64 restatement at the
+    GPU's ReLU decisions: every output within 1e-5 of max, every column of every dW within 1e-4
+    of that column's own max (the dw16 slab shifts are layer-wide, so a column far below the
+    layer's maximum would lose bits first), and every differing decision a tie."""
+    from fused_parity import FLIP_MARGIN, encoded_input, padded, run_fused
+    got = run_fused(engine, full, seed=1.0)
+    X = encoded_input(full, True)
+    ref = nerf_np.nerf_forward_backward_chunked(X, full.ws, full.bs, full.dists, full.target, full.S,
+                                                seed=1.0, masks=got["masks"], rays_per_chunk=256)
+    assert abs(got["loss"] - ref["loss"]) <= 1e-6 * ref["loss"]
+    assert_close("acc", got["acc"], ref["acc"], **TOL64)
+    assert_close("d_dists", got["d_dists"], ref["d_dists"], **TOL64)
+    assert_close("d_target", got["d_target"], ref["d_target"], **TOL64)
+    dW = padded(ref["dW"], full.wp.shape)
+    assert_close("dW", got["dW"], dW, **TOL64)
+    assert_close("dB", got["dB"], padded(ref["db"], full.bp.shape), **TOL64)
+    worst_col = 0.0
+    for l, (k, n) in enumerate(x.shape for x in full.ws):
+        want = dW[l, :k, :n]
+        err = np.abs(got["dW"][l, :k, :n] - want).max(axis=0)
+        cmax = np.abs(want).max(axis=0)
+        live = cmax > 0
+        worst_col = max(worst_col, float((err[live] / cmax[live]).max(initial=0.0)))
+    flips = sum(len(f) for f in ref["flip_margins"])
+    worst = max((float(f.max()) for f in ref["flip_margins"] if len(f)), default=0.0)
+    print(f"full size: {flips} decisions differ from float64 (worst |z|/T {worst:.3g}); "
+          f"worst per-column dW error {worst_col:.3g} of the column max")
+    assert worst <= FLIP_MARGIN
+    assert worst_col <= 1e-4, worst_col
+
+
 def test_full_size_oracle_rays_spotcheck(engine, full):
     """Per-ray outputs of the full batch for a few rays, against the oracle run on just those
     rays (acc_color and d_target depend only on their own ray)."""
@@ -263,7 +319,7 @@ def test_full_size_oracle_rays_spotcheck(engine, full):
 
 # ---- against the committed golden fixtures (float64 numpy restatement) ------------------------
 
-@pytest.mark.parametrize("prec", PRECISIONS)
+@pytest.mark.parametrize("prec", FUSED + ONE_WAVE)
 @pytest.mark.parametrize("name", ["chunk_4x30.npz", "deep8_w64_2x64.npz", "trained_weights_8x16.npz"])
 def test_fused_matches_golden_fixture(engine, name, prec):
     import os
@@ -279,13 +335,14 @@ def test_fused_matches_golden_fixture(engine, name, prec):
                           samples=S, input_mode=lnerf.INPUT_ENCODED, seed=1.0, want_per_ray=True,
                           want_dx=True, flags=lnerf.FAST | prec)
     torch.cuda.synchronize()
-    assert abs(float(r.loss.item()) - g["loss"]) <= 1e-5 * abs(g["loss"])
-    assert_close("acc", r.acc_color.cpu().numpy(), g["acc"], **TOL)
-    assert_close("dW", r.d_ws.cpu().numpy(), g["dW"], **TOL)
-    assert_close("dB", r.d_bs.cpu().numpy(), g["dB"], **TOL)
-    assert_close("dX", r.d_x.cpu().numpy(), g["dX"], **TOL)
-    assert_close("d_dists", r.d_dists.cpu().numpy(), g["d_dists"], **TOL)
-    assert_close("d_target", r.d_target.cpu().numpy(), g["d_target"], **TOL)
+    tol = TOL64 if prec in FUSED else _one_wave_tol(prec)
+    assert abs(float(r.loss.item()) - g["loss"]) <= 1e-6 * abs(g["loss"])
+    assert_close("acc", r.acc_color.cpu().numpy(), g["acc"], **tol)
+    assert_close("dW", r.d_ws.cpu().numpy(), g["dW"], **tol)
+    assert_close("dB", r.d_bs.cpu().numpy(), g["dB"], **tol)
+    assert_close("dX", r.d_x.cpu().numpy(), g["dX"], **tol)
+    assert_close("d_dists", r.d_dists.cpu().numpy(), g["d_dists"], **tol)
+    assert_close("d_target", r.d_target.cpu().numpy(), g["d_target"], **tol)
 
 
 def test_single_hip_runtime_mapped(engine):
@@ -440,54 +497,6 @@ def test_render_image_bf16_close_to_fp32_accurate(engine):
     want = oracle.standard_forward_backward(Xs, wp, bp, shapes, dists[sub],
                                             np.zeros((len(sub), 3), np.float32), 128, seed=1.0)
     assert_close("acc", a[sub], want["acc"], **TOL)
-
-
-# ---- kact (LNERF_KACT=1: activations in LDS, fp16x3 on 32x32x16 MFMAs) through the same checks --
-
-KACT_CASES = ["cfg2_points", "cfg2_encoded", "cfg3", "nonuniform", "deep", "ragged", "dx", "render", "rays",
-              "golden:chunk_4x30.npz", "golden:deep8_w64_2x64.npz", "golden:trained_weights_8x16.npz"]
-
-
-@pytest.mark.parametrize("case", KACT_CASES)
-def test_kact_matches_oracle(engine, case, monkeypatch):
-    """The opt-in kact kernel against the oracle / fixtures on the k16 tests' workloads, and the
-    path report proving it ran."""
-    monkeypatch.setenv("LNERF_KACT", "1")
-    if case == "cfg2_points":
-        test_fused_cfg2_matches_oracle(engine, True, 0)
-    elif case == "cfg2_encoded":
-        test_fused_cfg2_matches_oracle(engine, False, 0)
-    elif case == "cfg3":
-        test_fused_cfg3_subset_matches_oracle(engine, 0)
-    elif case == "nonuniform":
-        test_fused_nonuniform_widths(engine, 0)
-    elif case == "deep":
-        test_fused_deep_mlp(engine, 0)
-    elif case == "ragged":
-        test_fused_ragged_rays_and_samples(engine)
-    elif case == "dx":
-        test_fused_dx_encoded(engine)
-    elif case == "render":
-        test_render_forward_only_matches_train_forward(engine)
-    elif case == "rays":
-        test_rays_mode_matches_oracle(engine, False)
-    else:
-        test_fused_matches_golden_fixture(engine, case.split(":", 1)[1], 0)
-    assert engine.last_path()["kact"], engine.last_path()
-
-
-def test_kact_full_size_determinism_and_fused_vs_generic(engine, full_noties, monkeypatch):
-    """kact at the bench size: bitwise run-to-run determinism and parity with the loma-order
-    generic path on the tie-free rays."""
-    import lnerf
-    monkeypatch.setenv("LNERF_KACT", "1")
-    a = run_native(engine, full_noties, seed=1.0)
-    assert engine.last_path()["kact"]
-    a2 = run_native(engine, full_noties, seed=1.0)
-    for k in ("dW", "dB", "d_dists", "d_target"):
-        assert np.array_equal(a[k], a2[k]), k
-    b = run_native(engine, full_noties, seed=1.0, flags=lnerf.GENERIC)
-    compare(a, b)
 
 
 # ---- the training loop (train_nerf.py:325-499): loss-seeded step + Adam, on the device ----------

@@ -58,6 +58,8 @@ def parse():
                     help="fused path with exact f32 MFMA products instead of the bf16x6 split")
     ap.add_argument("--x6-train", action="store_true",
                     help="fused path with the bf16x6 split instead of the default fp16x3 split")
+    ap.add_argument("--k32", action="store_true",
+                    help="A/B: the 32-samples-per-wave k32 kernel in place of k16 (lnerf.K32)")
     ap.add_argument("--no-optimizer", action="store_true",
                     help="fwd+bwd only: skip the on-device Adam update (train_nerf.py:133-161) "
                          "that every timed step otherwise applies after the gradient exchange")
@@ -267,6 +269,8 @@ def main():
         flags |= lnerf.MFMA_F32
     elif args.x6_train:
         flags |= lnerf.MFMA_BF16X6
+    if args.k32:
+        flags |= lnerf.K32
 
     def step(timing=False):
         f = flags | (lnerf.TIMING if timing else 0)
@@ -345,7 +349,8 @@ def main():
             # the fused kernel the engine ran: k16 (wave pairs, the default) or the
             # one-wave-per-SIMD kernel (exact f32 MFMA / LNERF_ONE_WAVE)
             lp = eng.last_path()
-            k1 = "k16_fwd_bwd_kernel" if lp["k16"] else "fused_fwd_bwd_kernel"
+            k1 = ("k16_fwd_bwd_kernel" if lp["k16"] else "k32_fwd_bwd_kernel" if lp["k32"]
+                  else "fused_fwd_bwd_kernel")
             out["roofline"] = {"bound": "mfma", "kernel": k1,
                                "achieved": fused_flops / (fus_ms / 1e3) / 1e12,
                                "peak": peak, "unit": "TFLOP/s",

@@ -146,6 +146,8 @@ enum {
     LNERF_MFMA_BF16X6 = 512,  /* fused path: the bf16x6 split (x = hi+mid+lo in bf16, six bf16
                                  MFMAs per product, dropped terms <= 2^-24 |w x|); the default
                                  where k16 does not run (LNERF_ONE_WAVE, heads over 16 outputs) */
+    LNERF_K32 = 2048,         /* fused path: the k32 kernel (one wave per SIMD, 32 samples per
+                                 wave, 32x32x16 MFMAs) in place of k16                         */
     LNERF_ONE_WAVE = 1024     /* fused path: the one-wave-per-SIMD kernel pair
                                  (fused_fwd_bwd_kernel + dw_all_kernel) instead of k16 + dw16,
                                  for A/B runs; bf16x6 unless LNERF_MFMA_F32 / LNERF_MFMA_BF16.
@@ -207,7 +209,8 @@ enum {
     LNERF_PATH_GENERIC = 1,   /* the loma-order stage-by-stage kernels                        */
     LNERF_PATH_FUSED = 2,     /* the fused MFMA step (any kernel pair below)                  */
     LNERF_PATH_K16 = 4,       /* fused kernel on wave pairs (k16_fwd_bwd_kernel)              */
-    LNERF_PATH_DW16 = 8       /* dW kernel on wave pairs (dw16_kernel)                        */
+    LNERF_PATH_DW16 = 8,      /* dW kernel on wave pairs (dw16_kernel)                        */
+    LNERF_PATH_K32 = 16       /* fused kernel with one wave per SIMD (k32_fwd_bwd_kernel)     */
 };
 int lnerf_ctx_last_path(lnerf_ctx* ctx);
 

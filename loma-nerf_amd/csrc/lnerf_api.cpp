@@ -607,8 +607,8 @@ struct lnerf_ctx {
 };
 
 static int path_bits(const FusedPlan& p, bool train) {
-    return LNERF_PATH_FUSED | (p.k16 ? LNERF_PATH_K16 : 0) | (train && p.dw16 ? LNERF_PATH_DW16 : 0) |
-           (p.x6 << 8);
+    return LNERF_PATH_FUSED | (p.k16 ? LNERF_PATH_K16 : 0) | (p.k32 ? LNERF_PATH_K32 : 0) |
+           (train && p.dw16 ? LNERF_PATH_DW16 : 0) | (p.x6 << 8);
 }
 
 // At most one MFMA precision flag; fp16x3 only where k16 runs (it is k16's split).
@@ -618,7 +618,7 @@ static void check_precision_flags(int flags) {
 }
 static void check_plan_precision(const FusedPlan& p, int flags) {
     if ((flags & LNERF_MFMA_F16X3) && p.x6 != 2)
-        fail("LNERF_MFMA_F16X3 needs the k16 kernel (head <= 16 outputs, no LNERF_ONE_WAVE)");
+        fail("LNERF_MFMA_F16X3 needs the k16 / k32 kernel (head <= 16 outputs, no LNERF_ONE_WAVE)");
 }
 
 extern "C" const char* lnerf_last_error(void) { return g_last_error.c_str(); }
@@ -814,7 +814,7 @@ extern "C" int lnerf_train_step(lnerf_ctx* ctx, const lnerf_mlp* mlp, const floa
             ctx->timed = timed;
             ctx->last_path = path_bits(p, true);
             ctx->last_plan = p;
-            ctx->last_k16_train = p.k16 != 0;
+            ctx->last_k16_train = p.k16 != 0 || p.k32 != 0;
         } else {
             ctx->last_k16_train = false;
             generic_step(ctx, *mlp, ws, bs, *batch, seed, flags, o, true, s);
@@ -895,7 +895,8 @@ extern "C" int lnerf_ctx_relu_masks(lnerf_ctx* ctx, unsigned char* out, size_t o
         const size_t need = (size_t)(p.L - 1) * p.R * 32;
         if (out_bytes < need) fail("relu mask buffer holds %zu bytes, needs %zu", out_bytes, need);
         HIP_OK(hipSetDevice(ctx->device));
-        k16_masks_launch(p, out, (hipStream_t)stream);
+        if (p.k32) k32_masks_launch(p, out, (hipStream_t)stream);
+        else k16_masks_launch(p, out, (hipStream_t)stream);
         check_launch("lnerf_ctx_relu_masks");
     });
 }

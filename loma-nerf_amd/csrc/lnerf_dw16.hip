@@ -68,6 +68,7 @@ struct Dw16Args {
     int rpad;                   // slab positions per layer
     const int* eshift;          // per-layer product shift E_l (k1_reduce_kernel)
     int L;
+    int fmt;                    // slab tile layout: 0 = k16's, 1 = k32's (row_map)
 };
 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
@@ -78,15 +79,33 @@ __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane
 // n, with h = (t / 64) % 2 and n = (t % 64) / 4. A slab block is [tile][half-block 2][512]. The
 // per-thread part of the offset is fixed (RowMap), the half-block part is wave-uniform.
 struct RowMap {
-    int lane;        // per-thread float offset inside a tile's half-block: 4 (t % 128)
+    int lane;        // per-thread float offset inside a tile's half-block
+    int hstride;     // floats between the two half-blocks of a 32-sample block's tile
+    int rowo;        // the thread's first feature inside its 32-feature tile (4 consecutive)
+    int isamp;       // the thread's sample inside the half-block (its LDS image row)
     int tile[4];     // wave-uniform: the 32-feature tile of round i (tile 0 for tiles past the layer)
     bool ok[4];      // wave-uniform: the tile exists in this layer (else it is never split)
 };
 
-__device__ __forceinline__ RowMap row_map(int kt, int nt) {
+// fmt 0 (k16): a tile's half-block is [h 2][16 samples][16 features], thread t % 128 takes floats
+// 4 (t % 128)..+3 = features 16 h + 4 (t % 4) ..+3 of sample (t % 64) / 4, h = (t / 64) % 2.
+// fmt 1 (k32): a tile of a 32-sample block is [q 4][lane 64][4] with lane = 32 hh + sample, so
+// the half-block's part is 8 runs of 64 floats; thread u = t % 128 takes q = u / 32, hh =
+// (u / 16) % 2, sample u % 16: features 8 q + 4 hh ..+3.
+__device__ __forceinline__ RowMap row_map(int kt, int nt, int fmt) {
     RowMap m;
-    const int t = threadIdx.x;
-    m.lane = 4 * (t & 127);
+    const int t = threadIdx.x, u = t & 127;
+    if (fmt) {
+        m.lane = (u >> 5) * 256 + ((u >> 4) & 1) * 128 + (u & 15) * 4;
+        m.hstride = 64;
+        m.rowo = 8 * (u >> 5) + 4 * ((u >> 4) & 1);
+        m.isamp = u & 15;
+    } else {
+        m.lane = 4 * u;
+        m.hstride = 512;
+        m.rowo = 16 * ((t >> 6) & 1) + 4 * (t & 3);
+        m.isamp = (t & 63) >> 2;
+    }
     const int w2 = wave_id() >> 1;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -98,9 +117,8 @@ __device__ __forceinline__ RowMap row_map(int kt, int nt) {
 }
 
 // image feature row of round i's 4 values for thread t (A rows 0..255, G rows 256..511)
-__device__ __forceinline__ int image_row(int i) {
-    const int t = threadIdx.x;
-    return (i < 2 ? 0 : 256) + 32 * (4 * (i & 1) + (t >> 7)) + 16 * ((t >> 6) & 1) + 4 * (t & 3);
+__device__ __forceinline__ int image_row(int i, const RowMap& m) {
+    return (i < 2 ? 0 : 256) + 32 * (4 * (i & 1) + (threadIdx.x >> 7)) + m.rowo;
 }
 
 struct Loads {
@@ -135,10 +153,10 @@ __device__ __forceinline__ void issue_loads(const float* A, const float* G, cons
                                             int nt, const RowMap& m, int hb, int hb_end, Loads& L) {
     const bool in = hb < hb_end;
     const int hbc = in ? hb : max(0, hb_end - 1);
-    L.e = se[hbc * 16 + ((threadIdx.x & 63) >> 2)];
+    L.e = se[hbc * 16 + m.isamp];
     const int blk = hbc >> 1, half = hbc & 1;
-    const float* pa = A + (size_t)blk * kt * 1024 + half * 512;
-    const float* pg = G + (size_t)blk * nt * 1024 + half * 512;
+    const float* pa = A + (size_t)blk * kt * 1024 + half * m.hstride;
+    const float* pg = G + (size_t)blk * nt * 1024 + half * m.hstride;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const fx4* p = (const fx4*)((i < 2 ? pa : pg) + m.tile[i] * 1024 + m.lane);
@@ -173,9 +191,9 @@ __device__ __forceinline__ void split_h2(float x0, float x1, float sc, unsigned&
 // Split round i of the thread's values (4 features of sample n) into the plane image: 8 B per
 // plane at [plane][n][row .. row + 3]; rounds 0, 1 are A rows (shift ea), 2, 3 G rows (shift eg).
 template <int PL>
-__device__ __forceinline__ void write_planes_row(const fx4& v, int i, unsigned char* img, float sa, float sg) {
-    const int t = threadIdx.x;
-    unsigned char* p = img + ((t & 63) >> 2) * kImgRow + image_row(i) * 2;
+__device__ __forceinline__ void write_planes_row(const fx4& v, int i, unsigned char* img, float sa, float sg,
+                                                 const RowMap& m) {
+    unsigned char* p = img + m.isamp * kImgRow + image_row(i, m) * 2;
     const float sc = i < 2 ? sa : sg;
     if constexpr (PL == 2) {
         typedef unsigned u2 __attribute__((ext_vector_type(2)));
@@ -202,11 +220,11 @@ __device__ __forceinline__ void sample_scales(unsigned e, int E, float& sa, floa
 }
 
 template <int PL>
-__device__ __forceinline__ void write_planes(const Loads& L, unsigned char* img, int E) {
+__device__ __forceinline__ void write_planes(const Loads& L, unsigned char* img, int E, const RowMap& m) {
     float sa, sg;
     sample_scales(L.e, E, sa, sg);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) write_planes_row<PL>(L.v[i], i, img, sa, sg);
+    for (int i = 0; i < 4; ++i) write_planes_row<PL>(L.v[i], i, img, sa, sg, m);
 }
 
 __device__ __forceinline__ fx16 mfma32(const bf8& a, const bf8& b, fx16 c) {
@@ -260,7 +278,7 @@ __device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int 
     for (int k = 0; k < 4; ++k) {
         // rows past the layer's tiles are never read: skip their split (wave-uniform: a wave's
         // values of a round lie in one 32-feature tile); FULL layers need no branch
-        if (FULL || m.ok[k]) write_planes_row<PL>(nl.v[k], k, nxt, sa, sg);
+        if (FULL || m.ok[k]) write_planes_row<PL>(nl.v[k], k, nxt, sa, sg, m);
         if constexpr (ACTIVE) {
             if (k < TJ) {
                 const int j = k < TJ ? k : 0;
@@ -352,7 +370,7 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
 
     const float* A = a.act + a.a_off[l];
     const float* G = a.grad + a.g_off[l];
-    const RowMap m = row_map(KT, NT);
+    const RowMap m = row_map(KT, NT, a.fmt);
     // the per-sample balanced shifts (sample_shifts): every product carries 2^E, removed from the
     // partials at the end (exact)
     const unsigned short* se = a.sexp + (size_t)l * a.rpad;
@@ -365,7 +383,7 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
     if (hb0 < hb1) {
         dbs[0] += L0.v[2];
         dbs[1] += L0.v[3];
-        write_planes<PL>(L0, lds, E);
+        write_planes<PL>(L0, lds, E, m);
     }
     __syncthreads();
     if (active && full) hb_loop3<PL, TI, TJ, true, true>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
@@ -398,7 +416,7 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) red[(image_row(2 + i) - 256 + j) * 16 + ((tid & 63) >> 2)] = dbs[i][j];
+        for (int j = 0; j < 4; ++j) red[(image_row(2 + i, m) - 256 + j) * 16 + m.isamp] = dbs[i][j];
     __syncthreads();
     if (tid < NT * 32) {
         const float* q = red + tid * 16;
@@ -497,6 +515,7 @@ void dw16_launch(const FusedPlan& p, hipStream_t s) {
     a.sexp = (const unsigned short*)p.sexp;
     a.rpad = p.num_wg * 128;
     a.eshift = p.dw_shift;
+    a.fmt = p.k32 ? 1 : 0;
     a.L = p.L;
     // the per-layer product shifts of k1_reduce_launch (launched right after k1)
     if (p.x6 == 2) dw16_kernel<2><<<p.dw_grid, kThreads, 0, s>>>(a);
@@ -506,7 +525,8 @@ void dw16_launch(const FusedPlan& p, hipStream_t s) {
 
 void k1_reduce_launch(const FusedPlan& p, float* out_loss, hipStream_t s) {
     const int nl = p.dw16 ? p.L : 0;
-    k1_reduce_kernel<<<nl + 1, 1024, 0, s>>>(p.epart, p.num_wg * 8, p.dw_shift, nl, p.loss_part, p.num_wg,
+    // k1's per-wave minima: 8 waves per workgroup for k16, 4 for k32
+    k1_reduce_kernel<<<nl + 1, 1024, 0, s>>>(p.epart, p.num_wg * (p.k32 ? 4 : 8), p.dw_shift, nl, p.loss_part, p.num_wg,
                                              p.loss_total, out_loss);
 }
 

@@ -1479,6 +1479,8 @@ struct Layout {
     // k16 kernel packing (lnerf_k16.hip): 16-wide output tiles, 32-feature k-steps, 3 planes
     int ht16, ks16_f[kMaxLayers], ks16_b[kMaxLayers], to16_f[kMaxLayers], to16_b[kMaxLayers];
     size_t w16f_off[kMaxLayers], w16b_off[kMaxLayers], w16_total;   // u16
+    int ht32, to32_f[kMaxLayers], to32_b[kMaxLayers];                // k32: 32-wide output tiles
+    size_t w32f_off[kMaxLayers], w32b_off[kMaxLayers];               // u16, in the same region
     size_t b16_total;                                                 // floats
     size_t mask_total;                                                // u64 (k16 ReLU masks)
 };
@@ -1533,7 +1535,18 @@ void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S, bool train, int
         y.w16f_off[l] = off; off += align_up((size_t)y.ks16_f[l] * y.to16_f[l] * 3 * 512, 512);
         y.w16b_off[l] = off; off += align_up((size_t)y.ks16_b[l] * y.to16_b[l] * 3 * 512, 512);
     }
-    y.w16_total = off;
+    // k32 (lnerf_k32.hip): per input tile [2 k-steps][32-wide output tiles][planes][1 KiB]
+    int mx32 = 1;
+    for (int l = 0; l + 1 < L; ++l) mx32 = (m.n[l] + 31) / 32 > mx32 ? (m.n[l] + 31) / 32 : mx32;
+    y.ht32 = pow2_tiles(mx32);
+    size_t off32 = 0;
+    for (int l = 0; l < L; ++l) {
+        y.to32_f[l] = (l < L - 1) ? y.ht32 : 1;
+        y.to32_b[l] = (l >= 1) ? y.ht32 : pow2_tiles((m.k[0] + 31) / 32);
+        y.w32f_off[l] = off32; off32 += align_up((size_t)y.ks16_f[l] * 2 * y.to32_f[l] * 3 * 512, 512);
+        y.w32b_off[l] = off32; off32 += align_up((size_t)y.ks16_b[l] * 2 * y.to32_b[l] * 3 * 512, 512);
+    }
+    y.w16_total = off > off32 ? off : off32;
     y.b16_total = (size_t)L * 256;
     y.rpw = S >= kTileSamples ? 1 : kTileSamples / S;
     y.num_wg = (rays + y.rpw - 1) / y.rpw;
@@ -1709,11 +1722,19 @@ void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws
         p.to16_b[l] = y.to16_b[l];
         p.w16f_off[l] = y.w16f_off[l];
         p.w16b_off[l] = y.w16b_off[l];
+        p.to32_f[l] = y.to32_f[l];
+        p.to32_b[l] = y.to32_b[l];
+        p.w32f_off[l] = y.w32f_off[l];
+        p.w32b_off[l] = y.w32b_off[l];
     }
+    p.ht32 = y.ht32;
     p.k16 = k16_wanted && k16_supported(p) ? 1 : 0;
-    // dW: dw16_kernel after k16 (it reads k16's slab layout and fp16x3 / bf16x6 planes); the
+    // k32 (one wave per SIMD, 32 samples per wave) in place of k16 with LNERF_K32
+    p.k32 = p.k16 && (flags & LNERF_K32) && k32_supported(p) ? 1 : 0;
+    if (p.k32) p.k16 = 0;
+    // dW: dw16_kernel after k16 / k32 (it reads their slab layouts and split planes); the
     // one-wave kernel pairs with dw_all_kernel. One partial per split.
-    p.dw16 = p.k16;
+    p.dw16 = p.k16 || p.k32;
     if (p.dw16)
         for (int l = 0; l < p.L; ++l) p.dw_phases[l] = 1;
 }
@@ -1847,10 +1868,13 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
         if (ev) (void)hipEventRecord(ev[i], s);
     };
     mark(0);
-    if (p.k16) k16_pack(p, ws, bs, s);
+    if (p.k32) k32_pack(p, ws, bs, s);
+    else if (p.k16) k16_pack(p, ws, bs, s);
     else launch_pack(p, ws, bs, s);
     mark(1);
-    if (p.k16) {
+    if (p.k32) {
+        k32_launch(p, b, seed_loss ? 1.0f : seed, out, true, s);
+    } else if (p.k16) {
         k16_launch(p, b, seed_loss ? 1.0f : seed, out, true, s);
     } else {
         FusedArgs fa = make_fused_args(p, b, seed_loss ? 1.0f : seed, out, true);
@@ -1920,7 +1944,10 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
 
 void fused_render(const FusedPlan& p, const float* ws, const float* bs, const lnerf_batch& b,
                   const lnerf_outputs& out, hipStream_t s) {
-    if (p.k16) {
+    if (p.k32) {
+        k32_pack(p, ws, bs, s);
+        k32_launch(p, b, 1.0f, out, false, s);
+    } else if (p.k16) {
         k16_pack(p, ws, bs, s);
         k16_launch(p, b, 1.0f, out, false, s);
     } else {

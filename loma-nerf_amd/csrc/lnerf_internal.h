@@ -174,6 +174,11 @@ struct FusedPlan {
     float* b16;                          // [L][256] zero-padded biases
     unsigned long long* mask_g;          // [num_wg][L-1][8 waves][64 lanes] ReLU mask bits
     int dw16;                            // 1: dW by dw16_kernel (lnerf_dw16.hip), one partial per split
+    // k32 kernel (lnerf_k32.hip): 256-thread workgroups, one wave per SIMD, 32x32x16 MFMA
+    int k32;                             // 1: the fused step runs k32 (pack32 + k32 kernel)
+    int ht32;                            // 32-wide hidden output tiles (1/2/4/8)
+    int to32_f[kMaxLayers], to32_b[kMaxLayers];     // 32-wide output tiles per pass (input tiles: ks16_*)
+    size_t w32f_off[kMaxLayers], w32b_off[kMaxLayers];   // u16 offsets into w16
     int* wexp16;                         // x6 = 2: per-layer max|W| bits (fp16 weight plane shifts)
     int* wmax_part;                      // x6 = 2: max|W| bits per layer and wmax block [L][kWmaxParts]
     int* dw_shift;                       // dw16: per-layer product shift E_l (k1_reduce_kernel)
@@ -205,5 +210,11 @@ void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lner
                 bool want_grad, hipStream_t s);
 // the last training k1's ReLU decisions as (L-1, R, 32) bytes (lnerf_ctx_relu_masks)
 void k16_masks_launch(const FusedPlan& p, unsigned char* out, hipStream_t s);
+// k32 kernel entry points (lnerf_k32.hip)
+bool k32_supported(const FusedPlan& p);
+void k32_pack(const FusedPlan& p, const float* ws, const float* bs, hipStream_t s);
+void k32_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lnerf_outputs& out,
+                bool want_grad, hipStream_t s);
+void k32_masks_launch(const FusedPlan& p, unsigned char* out, hipStream_t s);
 
 }  // namespace lnerf

@@ -33,6 +33,7 @@ MFMA_BF16 = 128   # fused path: plain bf16 operands (reduced precision; inferenc
 MFMA_F16X3 = 256  # fused path: fp16x3 split (22-bit products, fp32 accumulate; the k16 default)
 MFMA_BF16X6 = 512  # fused path: bf16x6 split (fp32-accurate products)
 ONE_WAVE = 1024    # fused path: the one-wave-per-SIMD kernel pair instead of k16 + dw16 (A/B)
+K32 = 2048         # fused path: the 32-samples-per-wave 32x32 MFMA kernel instead of k16 (A/B)
 
 OPT_DW_GRID = 1    # lnerf_ctx_set_option: dW workgroups per step (0 = default 512)
 
@@ -50,6 +51,7 @@ PATH_GENERIC = 1
 PATH_FUSED = 2
 PATH_K16 = 4
 PATH_DW16 = 8
+PATH_K32 = 16
 
 
 class LnerfMLP(ctypes.Structure):
@@ -314,7 +316,8 @@ class Engine:
         if v < 0:
             raise RuntimeError(f"lnerf_ctx_last_path: {last_error()}")
         return dict(generic=bool(v & PATH_GENERIC), fused=bool(v & PATH_FUSED),
-                    k16=bool(v & PATH_K16), dw16=bool(v & PATH_DW16), planes=(v >> 8) & 3)
+                    k16=bool(v & PATH_K16), dw16=bool(v & PATH_DW16), k32=bool(v & PATH_K32),
+                    planes=(v >> 8) & 3)
 
     def relu_masks(self, L: int, R: int):
         """The last training step's hidden ReLU decisions (k16 path): numpy bool (L-1, R, 256),

@@ -67,6 +67,7 @@ def compare(got, want, keys=("dW", "dB", "d_dists", "d_target"), tol=TOL):
 
 
 FUSED = [0, 512]      # k16 + dw16: default fp16x3 split, lnerf.MFMA_BF16X6
+K32 = [2048, 2048 | 512]  # lnerf.K32 (32 samples per wave, 32x32 MFMA) + dw16: fp16x3, bf16x6
 ONE_WAVE = [64, 1024]  # one-wave pair: lnerf.MFMA_F32 (exact f32), lnerf.ONE_WAVE (bf16x6)
 
 
@@ -74,14 +75,14 @@ def _one_wave_tol(prec):
     return TOL_F32 if prec == 64 else TOL
 
 
-@pytest.mark.parametrize("prec", FUSED)
+@pytest.mark.parametrize("prec", FUSED + K32)
 @pytest.mark.parametrize("points", [True, False])
 def test_fused_cfg2_all_rays(engine, points, prec):
     """Config 2 (train_nerf-sized MLP 33->30->30->4), 1024 rays x 32 samples, seed = loss."""
     check_fused(engine, nerf_np.make_workload("cfg2"), points=points, flags=prec)
 
 
-@pytest.mark.parametrize("prec", FUSED)
+@pytest.mark.parametrize("prec", FUSED + K32)
 def test_fused_cfg3_subset_all_rays(engine, prec):
     """The bench MLP (33->256x7->4) on 48 rays x 64 samples, seed = loss."""
     check_fused(engine, nerf_np.make_workload("cfg3", rays=48), flags=prec)
@@ -110,7 +111,7 @@ def _nonuniform(w):
     return nerf_np.Workload(w.pts, w.pts32, w.X, w.dists, w.target, ws, bs, wp2, bp2, w.F, w.S, w.N)
 
 
-@pytest.mark.parametrize("prec", FUSED)
+@pytest.mark.parametrize("prec", FUSED + K32)
 def test_fused_nonuniform_widths(engine, prec):
     """Hidden widths that differ per layer (33->128->256->64->100->4): every layer's MMA runs
     with the widest layer's tile count over zero-padded packed weights."""
@@ -126,7 +127,7 @@ def _deep(w):
     return nerf_np.Workload(w.pts, w.pts32, w.X, w.dists, w.target, ws, bs, wp, bp, w.F, w.S, w.N)
 
 
-@pytest.mark.parametrize("prec", FUSED + ONE_WAVE + [128])
+@pytest.mark.parametrize("prec", FUSED + K32 + ONE_WAVE + [128])
 def test_fused_deep_mlp(engine, prec):
     """12 layers (33->64x11->4): the k16 kernel's chunk stream (2 passes x 11 hidden layers) and
     its HBM ReLU masks beyond the 8 hidden layers the one-wave kernel keeps in LDS. The bf16
@@ -134,22 +135,23 @@ def test_fused_deep_mlp(engine, prec):
     back to exact f32 past its mask budget (LNERF_ONE_WAVE too)."""
     import lnerf
     w = _deep(nerf_np.make_workload("cfg2", rays=32, samples=32))
-    if prec in FUSED:
+    if prec in FUSED + K32:
         check_fused(engine, w, flags=prec)
-        assert engine.last_path() == dict(generic=False, fused=True, k16=True, dw16=True,
-                                          planes={0: 2, 512: 3}[prec])
+        k32 = bool(prec & lnerf.K32)
+        assert engine.last_path() == dict(generic=False, fused=True, k16=not k32, dw16=True, k32=k32,
+                                          planes=3 if prec & lnerf.MFMA_BF16X6 else 2)
         return
     got = run_native(engine, nerf_np.without_relu_ties(w) if prec != 128 else w,
                      flags=lnerf.FAST | prec)
     path = engine.last_path()
     if prec == 128:
         # plain bf16 operands (8 significant bits): a loose sanity bound, not the fp32 tolerance
-        assert path == dict(generic=False, fused=True, k16=True, dw16=True, planes=1), path
+        assert path == dict(generic=False, fused=True, k16=True, dw16=True, k32=False, planes=1), path
         want = oracle_ref(w)
         assert abs(got["loss"] - want["loss"]) <= 2e-2 * abs(want["loss"]), (got["loss"], want["loss"])
         assert_close("dW", got["dW"], want["dW"], rtol=0.0, atol_scale=5e-2)
     else:
-        assert path == dict(generic=False, fused=True, k16=False, dw16=False, planes=0), path
+        assert path == dict(generic=False, fused=True, k16=False, dw16=False, k32=False, planes=0), path
         compare(got, oracle_ref(nerf_np.without_relu_ties(w)), tol=TOL_F32)
 
 
@@ -160,11 +162,12 @@ def test_default_path_is_k16_dw16(engine):
     import lnerf
     w = nerf_np.make_workload("cfg3", rays=8)
     run_native(engine, w, per_ray=False)
-    assert engine.last_path() == dict(generic=False, fused=True, k16=True, dw16=True, planes=2)
+    assert engine.last_path() == dict(generic=False, fused=True, k16=True, dw16=True, k32=False, planes=2)
     run_native(engine, w, per_ray=False, flags=lnerf.MFMA_F16X3)
     assert engine.last_path()["planes"] == 2
     run_native(engine, w, per_ray=False, flags=lnerf.ONE_WAVE)
-    assert engine.last_path() == dict(generic=False, fused=True, k16=False, dw16=False, planes=3)
+    assert engine.last_path() == dict(generic=False, fused=True, k16=False, dw16=False, k32=False,
+                                      planes=3)
     for bad in (lnerf.ONE_WAVE | lnerf.MFMA_F16X3, lnerf.MFMA_F16X3 | lnerf.MFMA_BF16X6,
                 lnerf.MFMA_BF16 | lnerf.MFMA_BF16X6):
         with pytest.raises(RuntimeError):
@@ -319,7 +322,7 @@ def test_full_size_oracle_rays_spotcheck(engine, full):
 
 # ---- against the committed golden fixtures (float64 numpy restatement) ------------------------
 
-@pytest.mark.parametrize("prec", FUSED + ONE_WAVE)
+@pytest.mark.parametrize("prec", FUSED + K32 + ONE_WAVE)
 @pytest.mark.parametrize("name", ["chunk_4x30.npz", "deep8_w64_2x64.npz", "trained_weights_8x16.npz"])
 def test_fused_matches_golden_fixture(engine, name, prec):
     import os
@@ -335,7 +338,7 @@ def test_fused_matches_golden_fixture(engine, name, prec):
                           samples=S, input_mode=lnerf.INPUT_ENCODED, seed=1.0, want_per_ray=True,
                           want_dx=True, flags=lnerf.FAST | prec)
     torch.cuda.synchronize()
-    tol = TOL64 if prec in FUSED else _one_wave_tol(prec)
+    tol = TOL64 if prec in FUSED + K32 else _one_wave_tol(prec)
     assert abs(float(r.loss.item()) - g["loss"]) <= 1e-6 * abs(g["loss"])
     assert_close("acc", r.acc_color.cpu().numpy(), g["acc"], **tol)
     assert_close("dW", r.d_ws.cpu().numpy(), g["dW"], **tol)

@@ -60,6 +60,10 @@ def parse():
                     help="fused path with the bf16x6 split instead of the default fp16x3 split")
     ap.add_argument("--k32", action="store_true",
                     help="A/B: the 32-samples-per-wave k32 kernel in place of k16 (lnerf.K32)")
+    ap.add_argument("--strong", action="store_true",
+                    help="config 4 strong scaling: one batch of the config's rays (4096) sharded "
+                         "over the ranks (contiguous ray ranges, 512 per GPU at N=8) instead of a "
+                         "full batch per GPU")
     ap.add_argument("--no-optimizer", action="store_true",
                     help="fwd+bwd only: skip the on-device Adam update (train_nerf.py:133-161) "
                          "that every timed step otherwise applies after the gradient exchange")
@@ -146,14 +150,8 @@ def bench_render(args, world, rank, local, dist):
     eng = lnerf.Engine(local)
     shapes, wp, bp = scene.init_mlp(3 + 6 * F, 4, L, H)
     mlp = lnerf.make_mlp(shapes, wp.shape[1], wp.shape[2])
-    # weights and biases packed like the gradient buffer [dW | db], so that one Adam launch
-    # updates both (padding entries have zero gradients and never move)
-    params = torch.cat([torch.from_numpy(wp).reshape(-1), torch.from_numpy(bp).reshape(-1)]).to(dev)
-    ws = params[:wp.size].view(wp.shape)
-    bs = params[wp.size:].view(bp.shape)
-    adam_m = torch.zeros_like(params)
-    adam_v = torch.zeros_like(params)
-    adam_t = [0]
+    ws = torch.from_numpy(wp).to(dev)
+    bs = torch.from_numpy(bp).to(dev)
     focal = 0.5 / np.tan(0.5 * scene.CAMERA_ANGLE_X)
     K = np.array([[focal, 0, 0.5], [0, focal, 0.5], [0, 0, 1]])
     rays_all = eng.get_rays(side, K, scene.look_at_pose())
@@ -239,7 +237,13 @@ def main():
             dist.destroy_process_group()
         return
     dev = f"cuda:{local}"
-    b = scene.make_batch(args.config, rays=args.rays, rank=rank)
+    if args.strong:
+        # config 4: ONE batch (the same rays on every rank), rank r takes its
+        # contiguous share (dp.shard_rays); the all-reduce SUM restores the whole batch's gradient
+        b = scene.shard_batch(scene.make_batch(args.config, rays=args.rays, rank=0),
+                              *dp.shard_rays(args.rays or scene.CONFIGS[args.config][1], world, rank))
+    else:
+        b = scene.make_batch(args.config, rays=args.rays, rank=rank)
     shapes, wp, bp = scene.init_mlp(3 + 6 * b["F"], 4, b["L"], b["H"])
     N, S = b["N"], b["S"]
     eng = lnerf.Engine(local)
@@ -307,7 +311,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     ms = dt / args.steps * 1e3
-    value = world * N * S / (ms / 1e3)
+    total_rays = b["N_total"] if args.strong else world * N
+    value = total_rays * S / (ms / 1e3)
 
     # per-kernel HIP-event times over extra timed steps (same stream, same kernels)
     kt = {}
@@ -327,13 +332,16 @@ def main():
         out = {
             "metric": METRIC, "value": value, "unit": "ray-samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": "strong" if args.strong else "weak",
+            "vs_baseline": None, "dtype": "f32",
             "mfma": ("generic (no MFMA)" if args.generic else "f32" if args.mfma_f32 else
                      "bf16x6 (fp32 operands split hi+mid+lo, fp32 accumulate)" if args.x6_train else
                      "fp16x3 (fp32 operands x 2^e split hi+lo in fp16, 3 products, fp32 accumulate)"),
             "data": "synthetic (look-at camera rays, uniform targets, random-init MLP seed 215)",
-            "config": {"workload": f"{args.config}: {N} rays x {S} samples per GPU, PE F={b['F']}, "
-                                   f"MLP {shapes[0][0]}->{b['H']}x{b['L'] - 1}->4, fp32",
+            "config": {"workload": (f"cfg4 (strong): one {total_rays}-ray x {S}-sample batch sharded "
+                                    f"over {world} GPU(s), {N} rays on rank 0" if args.strong else
+                                    f"{args.config}: {N} rays x {S} samples per GPU")
+                                   + f", PE F={b['F']}, MLP {shapes[0][0]}->{b['H']}x{b['L'] - 1}->4, fp32",
                        "rays_per_gpu": N, "samples": S, "layers": b["L"], "width": b["H"],
                        "parallelism": f"dp{world}", "path": "generic" if args.generic else "fused",
                        "optimizer": (None if args.no_optimizer else
@@ -362,13 +370,14 @@ def main():
                                               "products per fp32-accurate multiply-add)" if args.x6_train
                                               else "fp16 MFMA dense 2516.6 TF / 3 (fp16x3: three fp16 "
                                               "products per multiply-add)")}
-            tr = pmc_traffic(k1, args.config) if args.rays is None else None
+            full = args.rays is None and not args.strong
+            tr = pmc_traffic(k1, args.config) if full else None
             if tr:
                 out["roofline"]["traffic"] = tr["bytes"]
                 out["roofline"]["traffic_unit"] = "bytes/launch"
                 out["roofline"]["traffic_source"] = tr["source"]
                 out["roofline"]["traffic_gbs"] = tr["bytes"] / (fus_ms / 1e3) / 1e9
-            sq = sq_counters(k1) if args.rays is None and not (args.mfma_f32 or args.x6_train) else None
+            sq = sq_counters(k1) if full and not (args.mfma_f32 or args.x6_train) else None
             if sq:
                 out["roofline"]["mfma_busy"] = sq["mfma_busy"]
                 out["roofline"]["counters"] = sq

@@ -6,10 +6,10 @@
 #include <stdint.h>
 
 #include "lnerf.h"
+#include "lnerf_marshal.h"
 
 namespace lnerf {
 
-constexpr int kMaxLayers = LNERF_MAX_LAYERS;
 constexpr int kWmaxParts = 32;   // blocks per layer of the max|W| pass before the fp16x3 packing
 constexpr int kDefaultDwGrid = 512;   // dW workgroups per step unless LNERF_OPT_DW_GRID says otherwise
 
@@ -48,20 +48,6 @@ __host__ __device__ inline double ray_point(const float* ray6, int c, int j, int
 // Generic ("loma-order") path: one loma call on flat device rectangles. Field meaning follows
 // scripts/nerf.py:1-22; loop bounds are exactly the reference's.
 // ----------------------------------------------------------------------------------------------
-struct LgDims {
-    int L;                    // num_weights
-    int in_h, in_w;           // layer_input_h / layer_input_w
-    int th, tw;               // target_image_h / target_image_w
-    int S;                    // num_samples
-    int wsh1[kMaxLayers];     // weight_shapes[l][1]
-    int ios0[kMaxLayers];     // intermediate_output_shapes[l][0]
-    int ios1[kMaxLayers];     // intermediate_output_shapes[l][1]
-    int x_cols;               // strides of the flat rectangles
-    int w_k, w_n, b_n;
-    int io_rows, io_cols;
-    int t_cols, acc_cols;
-    int nerf_head;            // 1: nerf.py head (sigma ReLU on channel 3); 0: mlp_fit (all sigmoid)
-};
 
 struct LgBuffers {
     // primal (device)

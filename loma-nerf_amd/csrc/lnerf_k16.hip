@@ -306,12 +306,40 @@ __device__ __forceinline__ void read_tile(unsigned base, bf8 (&w)[3]) {
     if constexpr (PL == 3) w[2] = ds_read_at<(O * PL + 2) * 1024>(base);
 }
 
+// This wave's share of the next chunk's LDS-DMA, issued piece by piece between the MFMAs of the
+// first k-step of a chunk (LNERF_K16_SPREAD) instead of as one burst after the barrier, where
+// both waves of a SIMD would issue theirs together with no MFMA to hide behind. Piece p is the
+// wave instruction at byte wave * 1 KiB + p * 8 KiB of the chunk (1 KiB, lane-linear).
+#ifndef LNERF_K16_PRIO
+#define LNERF_K16_PRIO 0
+#endif
+#ifndef LNERF_K16_SPREAD
+#define LNERF_K16_SPREAD 1
+#endif
+constexpr int kPiecesMax = 8;   // pieces per wave of a full chunk (64 KiB / 8 waves)
+struct DmaJob {
+    const char* src = nullptr;   // this lane's address of piece 0
+    unsigned char* dst = nullptr;   // LDS address of this wave's piece 0
+    int n = 0;                   // this wave's pieces of the chunk
+};
+__device__ __forceinline__ void dma_piece(const DmaJob& j, int p) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(j.src + p * (kLoaders * 1024)),
+                                     (__attribute__((address_space(3))) void*)(j.dst + p * (kLoaders * 1024)), 16, 0,
+                                     0);
+}
+// the pieces that land on output tile O: p with p * NTO / kPiecesMax == O (all on tile 0 when NTO == 1)
+template <int NTO, int O, int... P>
+__device__ __forceinline__ void dma_pieces_at(const DmaJob& j, std::integer_sequence<int, P...>) {
+    (((P * NTO) / kPiecesMax == O ? (P < j.n ? dma_piece(j, P) : void()) : void()), ...);
+}
+
 // Output tile O of one k-step: issue the reads of tile O + kDist, wait for tile O's (leaving
 // the younger ones in flight), the MFMAs (small terms first).
 template <int NTO, int PL, int O>
 __device__ __forceinline__ void tile_step(unsigned base, bf8 (&w)[kDist + 1][3], const bf8& bh,
-                                          const bf8& bm, const bf8& bl, fx4 (&out)[kMaxT]) {
+                                          const bf8& bm, const bf8& bl, fx4 (&out)[kMaxT], const DmaJob& job) {
     if constexpr (O + kDist < NTO) read_tile<PL, O + kDist>(base, w[(O + kDist) % (kDist + 1)]);
+    if (job.n) dma_pieces_at<NTO, O>(job, std::make_integer_sequence<int, kPiecesMax>{});
     constexpr int ahead = (NTO - 1 - O) < kDist ? (NTO - 1 - O) : kDist;
     bf8(&c)[3] = w[O % (kDist + 1)];
     lgkm_wait<ahead * (LNERF_K16_HALFLDS && PL == 2 ? 1 : PL)>(c);
@@ -338,8 +366,8 @@ __device__ __forceinline__ void tile_step(unsigned base, bf8 (&w)[kDist + 1][3],
 template <int NTO, int PL, int B, int... O>
 __device__ __forceinline__ void tile_steps(std::integer_sequence<int, O...>, unsigned base,
                                            bf8 (&w)[kDist + 1][3], const bf8& bh, const bf8& bm,
-                                           const bf8& bl, fx4 (&out)[kMaxT]) {
-    (tile_step<NTO, PL, B + O>(base, w, bh, bm, bl, out), ...);
+                                           const bf8& bl, fx4 (&out)[kMaxT], const DmaJob& job) {
+    (tile_step<NTO, PL, B + O>(base, w, bh, bm, bl, out, job), ...);
 }
 
 // The B operand planes of k-step s (the lane's 8 input features phi(s, g, 0..7) of its sample):
@@ -395,16 +423,35 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
     const int lane = threadIdx.x & 63;
     const unsigned base = lds_addr(ring + (ci % R::slots) * R::slot_bytes) + kk * NTO * PL * 1024 + lane * 16;
     const bool st = slab && !LNERF_K16_NOSTORE;
+    constexpr bool spread = LNERF_K16_SPREAD && !R::stagger;
+    DmaJob job;
     if (kk == 0) {
-        // DMA of chunk ci + 1 first (its table entry is a scalar load the compiler waits for
-        // with lgkmcnt(0), which would also wait for the fragment reads), then the first weight
-        // tiles, in flight while the slab stores and the operand split issue. The barrier waits
-        // for this wave's pieces of chunk ci + 1 only: the slab stores issued after them (two
-        // per k-step) stay in flight.
-        const int issued = (LNERF_K16_NODMA && ci >= 2)
-                               ? 0
-                               : dma_chunk(a, chunk_at(a, ci + 1),
-                                           ring + ((ci + 1) % R::slots) * R::slot_bytes, bias_ring);
+        // DMA of chunk ci + 1 (its table entry is a scalar load the compiler waits for with
+        // lgkmcnt(0), so it is read before the fragment reads are issued). Unspread: every piece
+        // now, before the first weight tiles; spread: one piece per kPiecesMax-th of the output
+        // tiles, between the MFMAs. The barrier waits for this wave's pieces of chunk ci + 1 only:
+        // the slab stores issued after them (two per k-step) stay in flight.
+        const ChunkT c = (LNERF_K16_NODMA && ci >= 2) ? ChunkT{nullptr, 0, -1} : chunk_at(a, ci + 1);
+        unsigned char* dst = ring + ((ci + 1) % R::slots) * R::slot_bytes;
+        int issued;
+        if constexpr (spread) {
+            const int wave = wave_id();
+            const int woff = wave * 1024;
+            job.n = (c.src && woff < c.bytes) ? (c.bytes - woff + kLoaders * 1024 - 1) / (kLoaders * 1024) : 0;
+            job.src = (const char*)c.src + woff + lane * 16;
+            job.dst = dst + woff;
+            // the biases of a first forward chunk: one more piece from the last wave, now
+            issued = job.n;
+            if (c.bias >= 0 && wave == kLoaders - 1) {
+                const float* g = a.b16 + (size_t)c.bias * 256 + lane * 4;
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                                 (__attribute__((address_space(3))) void*)(bias_ring + (c.bias % 3) * 256),
+                                                 16, 0, 0);
+                ++issued;
+            }
+        } else {
+            issued = dma_chunk(a, c, dst, bias_ring);
+        }
         asm volatile("" ::: "memory");   // the slab stores stay younger than the pieces
         pending = issued ? 0 : -1;
     }
@@ -414,15 +461,20 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
     read_tile<PL, 0>(base, w[0]);
     if constexpr (NTO > 1) read_tile<PL, 1>(base, w[1]);
     static_assert(kDist == 2, "the prologue reads kDist tiles");
-    if (st) store_slab_step(slab + s * 1024, in[2 * s], in[2 * s + 1]);
+    if (st && !spread) store_slab_step(slab + s * 1024, in[2 * s], in[2 * s + 1]);
     // first half of the output tiles, [late waves: barrier], the next k-step's operand split (off
-    // the next prologue's critical path), second half, [early: barrier]
+    // the next prologue's critical path), second half, [spread: the slab stores, younger than
+    // every piece], [early: barrier]
     constexpr int H = (NTO + 1) / 2;
-    tile_steps<NTO, PL, 0>(std::make_integer_sequence<int, H>{}, base, w, bh, bm, bl, out);
+    tile_steps<NTO, PL, 0>(std::make_integer_sequence<int, H>{}, base, w, bh, bm, bl, out, job);
     if (late && last) dma_barrier(pending);
     bf8 nh = {}, nm = {}, nl = {};
     if (s + 1 < ks) make_b<PL>(in, s + 1 < 8 ? s + 1 : 0, ex, nh, nm, nl);
-    tile_steps<NTO, PL, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, bh, bm, bl, out);
+    tile_steps<NTO, PL, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, bh, bm, bl, out, job);
+    if (st && spread) {
+        asm volatile("" ::: "memory");
+        store_slab_step(slab + s * 1024, in[2 * s], in[2 * s + 1]);
+    }
     if (!late && last) dma_barrier(pending);
     if (last) ++ci;
     bh = nh;
@@ -561,6 +613,10 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
     const int wg = blockIdx.x;
     const int tile_samples = a.rpw * a.S;
     const int ls = wave * 16 + n;                      // local sample 0..127
+#if LNERF_K16_PRIO
+    // static priority for the second-dispatched half (MI355X_MICROARCH.md, two waves per SIMD 4)
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
     const int gs = wg * tile_samples + ls;             // global sample row (ray*S + j)
     const bool valid = (ls < tile_samples) && (gs < a.R);
     const size_t blk = (size_t)wg * 4 + (wave >> 1);   // 32-sample slab block

@@ -82,6 +82,16 @@ def make_batch(name="cfg3", rays=None, samples=None, rank=0):
                 rays=rays, target=target, F=F, S=S, N=N, L=L, H=H)
 
 
+def shard_batch(b, lo, hi):
+    """Rays [lo, hi) of a make_batch() batch (config 4 strong scaling: one batch split over the
+    ranks by dp.shard_rays). N_total keeps the whole batch's ray count."""
+    S = b["S"]
+    out = dict(b)
+    out.update(pts=b["pts"][lo * S:hi * S], dists=b["dists"][lo:hi], rays=b["rays"][lo:hi],
+               target=b["target"][lo:hi], N=hi - lo, N_total=b["N"])
+    return out
+
+
 def compute_psnr(img1, img2, max_val=1.0):
     """train_nerf.py:163-183: 20 log10(max / sqrt(mean((img1 - img2)^2))), numpy or torch."""
     mse = ((img1 - img2) ** 2).mean()

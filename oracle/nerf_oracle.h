@@ -91,6 +91,26 @@ float oracle_train_step(int L, const int* k_dims, const int* n_dims, int w_k, in
                         const float* X, int rays, int S, const float* dists, const float* T,
                         const float* W, const float* B, float* dW, float* dB, int threads);
 
+/* The two loma entry points above behind the reference's own nested-pointer ABI (SURVEY.md §8b;
+ * nerf_oracle_abi.c): gather the touched rows, run the flat oracle, scatter back. For timing the
+ * reference's per-chunk call pair on the CPU through the same tables the GPU library gets. */
+float oracle_abi_nerf_evaluate_and_march(float** layer_input, int layer_input_h, int layer_input_w,
+                                         float*** ws, float** bs, float** target_image, int target_image_h,
+                                         int target_image_w, int num_weights, int** weight_shapes,
+                                         int** bias_shapes, int** intermediate_output_shapes,
+                                         float*** intermediate_outputs, float*** img_sample_rgba_arr,
+                                         int num_samples, float** dists, float** alpha, float** cumprod_alpha,
+                                         float** weights_samples, float** accumulated_color);
+void oracle_abi_grad_nerf_evaluate_and_march(
+    float** layer_input, float** d_layer_input, int layer_input_h, int* d_h, int layer_input_w, int* d_w,
+    float*** ws, float*** d_ws, float** bs, float** d_bs, float** target_image, float** d_target,
+    int target_image_h, int* d_th, int target_image_w, int* d_tw, int num_weights, int* d_nw,
+    int** weight_shapes, int** d_wsh, int** bias_shapes, int** d_bsh, int** intermediate_output_shapes,
+    int** d_ios, float*** intermediate_outputs, float*** d_io, float*** img_sample_rgba_arr, float*** d_rgba,
+    int num_samples, int* d_ns, float** dists, float** d_dists, float** alpha, float** d_alpha,
+    float** cumprod_alpha, float** d_cumprod, float** weights_samples, float** d_wsamp,
+    float** accumulated_color, float** d_acc, float dreturn);
+
 #ifdef __cplusplus
 }
 #endif

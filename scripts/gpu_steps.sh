@@ -1,7 +1,7 @@
 # One GPU session = a list of named steps, each under its own time limit, stopping at the first
 # failure (a fault, abort, time limit or failing test ends the call):
 #   gpurun -- bash scripts/gpu_steps.sh tests bench trace sq
-# steps: tests | bench | k32 | k32trace | render | precision | trace | pmc | sq | compat
+# steps: tests | bench | k32 | k32trace | dist | render | precision | trace | pmc | sq | compat
 # Logs go to gpurun_out/<step>.log; rocprof output under gpurun_out/prof and gpurun_out/sq.
 set -u
 cd "$GRAFT_REPO_ROOT"
@@ -28,6 +28,17 @@ for step in "$@"; do
         -d "$R/gpurun_out/prof/k32trace" -o run -- python3 "$R/bench.py" --k32 --steps 10 --warmup 3 \
         --no-cpu-baseline > "$R/gpurun_out/prof/k32trace.log" 2>&1)
       rc=$? ;;
+    dist)
+      timeout -k 10 300 python -u -m pytest tests/test_gpu_dist.py -m gpu -x -v -p no:cacheprovider \
+        --timeout 120 --timeout-method thread > gpurun_out/dist.log 2>&1 &&
+      timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+        --master-addr 127.0.0.1 --master-port 29517 bench.py --no-cpu-baseline \
+        > gpurun_out/dist_weak.log 2>&1 &&
+      timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+        --master-addr 127.0.0.1 --master-port 29518 bench.py --strong --no-cpu-baseline \
+        > gpurun_out/dist_strong.log 2>&1
+      rc=$?; tail -3 gpurun_out/dist.log; tail -1 gpurun_out/dist_weak.log | cut -c1-400
+      tail -1 gpurun_out/dist_strong.log | cut -c1-400 ;;
     render)
       timeout -k 10 300 python bench.py --render --steps 5 --warmup 2 > gpurun_out/render.log 2>&1
       rc=$?; tail -1 gpurun_out/render.log | cut -c1-500 ;;

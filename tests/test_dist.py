@@ -108,3 +108,18 @@ def test_shard_rays_partitions():
             assert spans[0][0] == 0 and spans[-1][1] == n
             for (a, b), (c, d) in zip(spans, spans[1:]):
                 assert b == c
+
+
+def test_strong_scaling_shards_cover_one_batch():
+    """bench.py --strong (config 4): the ranks' shards of one batch concatenate to that batch."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "loma-nerf_amd"))
+    import dp
+    import scene
+    b = scene.make_batch("cfg2", rays=37)
+    for world in (1, 2, 8):
+        parts = [scene.shard_batch(b, *dp.shard_rays(b["N"], world, r)) for r in range(world)]
+        assert sum(p["N"] for p in parts) == b["N"] and all(p["N_total"] == b["N"] for p in parts)
+        for k in ("pts", "dists", "rays", "target"):
+            assert np.array_equal(np.concatenate([p[k] for p in parts]), b[k]), k

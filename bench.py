@@ -60,6 +60,8 @@ def parse():
                     help="fused path with the bf16x6 split instead of the default fp16x3 split")
     ap.add_argument("--k32", action="store_true",
                     help="A/B: the 32-samples-per-wave k32 kernel in place of k16 (lnerf.K32)")
+    ap.add_argument("--k16-w4", action="store_true",
+                    help="A/B: k16 on 4-wave 64-sample workgroups, two per CU (lnerf.K16_W4)")
     ap.add_argument("--strong", action="store_true",
                     help="config 4 strong scaling: one batch of the config's rays (4096) sharded "
                          "over the ranks (contiguous ray ranges, 512 per GPU at N=8) instead of a "
@@ -275,6 +277,8 @@ def main():
         flags |= lnerf.MFMA_BF16X6
     if args.k32:
         flags |= lnerf.K32
+    if args.k16_w4:
+        flags |= lnerf.K16_W4
 
     def step(timing=False):
         f = flags | (lnerf.TIMING if timing else 0)

@@ -148,6 +148,17 @@ enum {
                                  where k16 does not run (LNERF_ONE_WAVE, heads over 16 outputs) */
     LNERF_K32 = 2048,         /* fused path: the k32 kernel (one wave per SIMD, 32 samples per
                                  wave, 32x32x16 MFMAs) in place of k16                         */
+    LNERF_HEAD_FIT = 8192,    /* the mlp_fit head instead of the NeRF one (scripts/mlp_fit.py:
+                                 120-145, fit_img.py:423-532): sigmoid on every output channel,
+                                 loss = sum over rows x outputs of (sigmoid(z) - target)^2, no
+                                 compositing. samples must be 1 (a "ray" is one row of the
+                                 image), input ENCODED (rows, k[0]), target (rows, n_out) with
+                                 1 <= n_out <= 4, dists unused; acc_color receives the sigmoid
+                                 outputs (rows, n_out) and d_target (rows, n_out). Runs on k16
+                                 only (LNERF_GENERIC / LNERF_ONE_WAVE / LNERF_K32 are errors). */
+    LNERF_K16_W4 = 4096,      /* fused path: k16 on 4-wave, 64-sample workgroups (two per CU)
+                                 instead of 8-wave, 128-sample ones (samples <= 64, fp16x3 or
+                                 plain bf16; A/B -- measured slower at cfg3)                   */
     LNERF_ONE_WAVE = 1024     /* fused path: the one-wave-per-SIMD kernel pair
                                  (fused_fwd_bwd_kernel + dw_all_kernel) instead of k16 + dw16,
                                  for A/B runs; bf16x6 unless LNERF_MFMA_F32 / LNERF_MFMA_BF16.
@@ -210,7 +221,8 @@ enum {
     LNERF_PATH_FUSED = 2,     /* the fused MFMA step (any kernel pair below)                  */
     LNERF_PATH_K16 = 4,       /* fused kernel on wave pairs (k16_fwd_bwd_kernel)              */
     LNERF_PATH_DW16 = 8,      /* dW kernel on wave pairs (dw16_kernel)                        */
-    LNERF_PATH_K32 = 16       /* fused kernel with one wave per SIMD (k32_fwd_bwd_kernel)     */
+    LNERF_PATH_K32 = 16,      /* fused kernel with one wave per SIMD (k32_fwd_bwd_kernel)     */
+    LNERF_PATH_K16_W4 = 32    /* k16 on 4-wave, 64-sample workgroups (two per CU)             */
 };
 int lnerf_ctx_last_path(lnerf_ctx* ctx);
 

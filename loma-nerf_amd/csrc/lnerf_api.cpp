@@ -471,6 +471,7 @@ struct lnerf_ctx {
 
 static int path_bits(const FusedPlan& p, bool train) {
     return LNERF_PATH_FUSED | (p.k16 ? LNERF_PATH_K16 : 0) | (p.k32 ? LNERF_PATH_K32 : 0) |
+           (p.k16 && p.tile == 64 ? LNERF_PATH_K16_W4 : 0) |
            (train && p.dw16 ? LNERF_PATH_DW16 : 0) | (p.x6 << 8);
 }
 
@@ -518,7 +519,6 @@ static void validate(const lnerf_mlp* m, const lnerf_batch* b) {
         if (m->k[l] > m->w_k || m->n[l] > m->w_n) fail("layer %d exceeds padded layout", l);
         if (l > 0 && m->k[l] != m->n[l - 1]) fail("k[%d] != n[%d]", l, l - 1);
     }
-    if (m->n[m->num_layers - 1] < 4) fail("head needs >= 4 outputs");
     if (b->rays < 1 || b->samples < 1) fail("empty batch");
     if (!b->x || !b->target) fail("null batch pointer");
     if (b->input_mode == LNERF_INPUT_POINTS || b->input_mode == LNERF_INPUT_RAYS) {
@@ -527,7 +527,20 @@ static void validate(const lnerf_mlp* m, const lnerf_batch* b) {
     } else if (b->input_mode != LNERF_INPUT_ENCODED) {
         fail("unknown input_mode");
     }
-    if (b->input_mode != LNERF_INPUT_RAYS && !b->dists) fail("null dists");
+}
+
+// NeRF head (rgb + sigma) needs dists (unless RAYS) and >= 4 outputs; the mlp_fit head
+// (LNERF_HEAD_FIT) runs only on the fused k16 path, one row per "ray", without dists.
+static void validate_head(const lnerf_mlp* m, const lnerf_batch* b, int flags) {
+    if (!(flags & LNERF_HEAD_FIT)) {
+        if (m->n[m->num_layers - 1] < 4) fail("head needs >= 4 outputs");
+        if (b->input_mode != LNERF_INPUT_RAYS && !b->dists) fail("null dists");
+        return;
+    }
+    if (flags & (LNERF_GENERIC | LNERF_ONE_WAVE | LNERF_K32 | LNERF_MFMA_F32 | LNERF_MFMA_BF16X6))
+        fail("LNERF_HEAD_FIT runs on the k16 kernel only");
+    if (b->samples != 1 || b->input_mode != LNERF_INPUT_ENCODED || m->n[m->num_layers - 1] > 4)
+        fail("LNERF_HEAD_FIT needs samples == 1, ENCODED input and 1..4 outputs");
 }
 
 extern "C" size_t lnerf_workspace_bytes(const lnerf_mlp* mlp, int rays, int samples) {
@@ -647,7 +660,9 @@ static void generic_step(lnerf_ctx* ctx, const lnerf_mlp& m, const float* ws, co
 static bool use_fused(const lnerf_mlp& m, const lnerf_batch& b, int flags) {
     if (flags & LNERF_GENERIC) return false;
     const char* why = nullptr;
-    const bool ok = fused_supported(m, b.rays, b.samples, b.input_mode, &why);
+    const bool fit = (flags & LNERF_HEAD_FIT) != 0;
+    const bool ok = fused_supported(m, b.rays, b.samples, b.input_mode, &why, fit);
+    if (fit && !ok) fail("mlp_fit head: %s", why);
     if (!ok && (flags & LNERF_FAST)) fail("fused path unavailable: %s", why);
     if (ok && (flags & LNERF_WANT_DX) && b.input_mode != LNERF_INPUT_ENCODED)
         fail("LNERF_WANT_DX needs ENCODED input");
@@ -660,9 +675,11 @@ extern "C" int lnerf_train_step(lnerf_ctx* ctx, const lnerf_mlp* mlp, const floa
     return guard_int([&]() {
         if (!ctx) fail("null ctx");
         validate(mlp, batch);
+        validate_head(mlp, batch, flags);
         if (!ws || !bs) fail("null weights");
         lnerf_outputs o = out ? *out : lnerf_outputs{};
         if (!(flags & LNERF_WANT_DX)) o.d_x = nullptr;
+        if (flags & LNERF_HEAD_FIT) o.d_dists = nullptr;
         check_precision_flags(flags);
         std::lock_guard<std::mutex> lock(ctx->mu);
         HIP_OK(hipSetDevice(ctx->device));
@@ -703,6 +720,7 @@ extern "C" int lnerf_render(lnerf_ctx* ctx, const lnerf_mlp* mlp, const float* w
     return guard_int([&]() {
         if (!ctx) fail("null ctx");
         validate(mlp, batch);
+        validate_head(mlp, batch, flags);
         lnerf_outputs o = out ? *out : lnerf_outputs{};
         check_precision_flags(flags);
         std::lock_guard<std::mutex> lock(ctx->mu);

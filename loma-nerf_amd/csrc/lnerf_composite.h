@@ -196,5 +196,51 @@ __device__ __forceinline__ float composite_tile(const A& a, int wg, float* comp,
     return 0.0f;
 }
 
+// ---- the mlp_fit head (scripts/mlp_fit.py:120-145, fit_img.py:423-532) for one tile ----------
+// One thread per row (S = 1, so a "ray" is a row): sigmoid on each of the nout <= 4 head outputs
+// (mlp_fit.py:127-132: 1 / (1 + exp(0 - x))), loss = sum_c (o_c - t_c)^2 (mlp_fit.py:140-145;
+// the rows' partial sums are added in a tree by the caller instead of loma's sequential loop),
+// and its reverse with loma's adjoint expressions: d_o = 0 + a1 + a1 with a1 = (o - t) seed
+// (the two reads of the squared difference), d_target = (0 + a2) + a2, a2 = 0 - (o - t) seed,
+// then the sigmoid's Div/exp/Sub reverse on the pre-activation (lg_act_bwd_kernel's form).
+// LDS as composite_tile: comp[0..512) z [128][4] in, [512..1024) gz [128][4] out. `nout` is the
+// head width; a.target / a.acc_color / a.d_target are (rows, nout).
+template <class A>
+__device__ __forceinline__ float fit_tile(const A& a, int wg, float* comp, float* rayloss, bool grad, int nout) {
+    const int tid = threadIdx.x;
+    float* c_z = comp;
+    float* c_gz = comp + 512;
+    const int ls = tid < kTileSamples ? tid : kTileSamples;
+    const int row = wg * a.rpw + ls;
+    const bool valid = ls < a.rpw && row < a.rays;
+    float loss = 0.0f;
+    if (valid) {
+        const float* t = a.target + (size_t)row * nout;
+        for (int k = 0; k < nout; ++k) {
+            const float x = c_z[ls * 4 + k];
+            const float o = 1.0f / (1.0f + expf(0.0f - x));
+            loss = loss + (o - t[k]) * (o - t[k]);
+            if (a.acc_color) a.acc_color[(size_t)row * nout + k] = o;
+            if (grad) {
+                const float a1 = (o - t[k]) * a.seed;
+                const float a2 = 0.0f - ((o - t[k]) * a.seed);
+                const float dz = 0.0f + a1 + a1;
+                if (a.d_target) a.d_target[(size_t)row * nout + k] = (0.0f + a2) + a2;
+                const float u = 1.0f + expf(0.0f - x);
+                const float adj_div = ((0.0f - dz) * 1.0f) / (u * u);
+                c_gz[ls * 4 + k] = 0.0f + (0.0f - adj_div * expf(0.0f - x));
+            }
+        }
+        if (grad)
+            for (int k = nout; k < 4; ++k) c_gz[ls * 4 + k] = 0.0f;
+    } else if (grad && ls < kTileSamples) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) c_gz[ls * 4 + k] = 0.0f;
+    }
+    if (ls < a.rpw) rayloss[ls] = loss;
+    __syncthreads();
+    return 0.0f;
+}
+
 }  // namespace comp
 }  // namespace lnerf

@@ -513,7 +513,7 @@ void dw16_launch(const FusedPlan& p, hipStream_t s) {
     a.dw_part = p.dw_part;
     a.db_part = p.db_part;
     a.sexp = (const unsigned short*)p.sexp;
-    a.rpad = p.num_wg * 128;
+    a.rpad = p.num_wg * p.tile;
     a.eshift = p.dw_shift;
     a.fmt = p.k32 ? 1 : 0;
     a.L = p.L;
@@ -526,7 +526,7 @@ void dw16_launch(const FusedPlan& p, hipStream_t s) {
 void k1_reduce_launch(const FusedPlan& p, float* out_loss, hipStream_t s) {
     const int nl = p.dw16 ? p.L : 0;
     // k1's per-wave minima: 8 waves per workgroup for k16, 4 for k32
-    k1_reduce_kernel<<<nl + 1, 1024, 0, s>>>(p.epart, p.num_wg * (p.k32 ? 4 : 8), p.dw_shift, nl, p.loss_part, p.num_wg,
+    k1_reduce_kernel<<<nl + 1, 1024, 0, s>>>(p.epart, p.num_wg * (p.k32 ? 4 : p.tile / 16), p.dw_shift, nl, p.loss_part, p.num_wg,
                                              p.loss_total, out_loss);
 }
 

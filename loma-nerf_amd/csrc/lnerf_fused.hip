@@ -1488,7 +1488,8 @@ struct Layout {
 inline int pow2_tiles(int t) { return t <= 1 ? 1 : t <= 2 ? 2 : t <= 4 ? 4 : 8; }
 
 // train = false (render): no slabs or dW partials (the forward-only kernel writes none).
-void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S, bool train, int dw_grid) {
+void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S, bool train, int dw_grid,
+                 int tile = kTileSamples) {
     const int L = m.num_layers;
     int kt[kMaxLayers], nt[kMaxLayers];
     for (int l = 0; l < L; ++l) {
@@ -1548,10 +1549,10 @@ void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S, bool train, int
     }
     y.w16_total = off > off32 ? off : off32;
     y.b16_total = (size_t)L * 256;
-    y.rpw = S >= kTileSamples ? 1 : kTileSamples / S;
+    y.rpw = S >= tile ? 1 : tile / S;
     y.num_wg = (rays + y.rpw - 1) / y.rpw;
-    y.mask_total = train ? (size_t)y.num_wg * (L > 1 ? L - 1 : 0) * 8 * 64 : 0;
-    y.blocks = y.num_wg * kWaves;
+    y.mask_total = train ? (size_t)y.num_wg * (L > 1 ? L - 1 : 0) * (tile / 16) * 64 : 0;
+    y.blocks = y.num_wg * (tile / 32);
     off = 0;
     y.x_off = off; off += (size_t)y.blocks * kt[0] * 1024;
     for (int l = 0; l < L - 1; ++l) { y.act_off[l] = off; off += (size_t)y.blocks * nt[l] * 1024; }
@@ -1591,12 +1592,14 @@ void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S, bool train, int
 
 }  // namespace
 
-bool fused_supported(const lnerf_mlp& m, int rays, int S, int input_mode, const char** why) {
+bool fused_supported(const lnerf_mlp& m, int rays, int S, int input_mode, const char** why, bool head_fit) {
     const char* w = nullptr;
     if (m.num_layers < 1 || m.num_layers > kMaxLayers) w = "num_layers out of range";
     else if (S < 1 || S > kTileSamples) w = "fused path needs 1 <= samples <= 128";
     else if (rays < 1) w = "no rays";
-    else if (m.n[m.num_layers - 1] < 4) w = "head must have >= 4 outputs (rgb + sigma)";
+    else if (head_fit && (S != 1 || m.n[m.num_layers - 1] > 4 || input_mode != LNERF_INPUT_ENCODED))
+        w = "the mlp_fit head needs samples == 1, 1..4 outputs and ENCODED input";
+    else if (!head_fit && m.n[m.num_layers - 1] < 4) w = "head must have >= 4 outputs (rgb + sigma)";
     else if (m.n[m.num_layers - 1] > 32) w = "fused path needs a head with <= 32 outputs";
     else {
         for (int l = 0; l < m.num_layers && !w; ++l) {
@@ -1611,24 +1614,35 @@ bool fused_supported(const lnerf_mlp& m, int rays, int S, int input_mode, const 
     return w == nullptr;
 }
 
-size_t fused_workspace_bytes(const lnerf_mlp& m, int rays, int S, bool train, int dw_grid) {
+static size_t workspace_floats(const lnerf_mlp& m, int rays, int S, bool train, int dw_grid, int tile) {
     Layout y;
-    make_layout(y, m, rays, S, train, dw_grid);
+    make_layout(y, m, rays, S, train, dw_grid, tile);
     size_t f = align_up(y.pack_total, 64) + align_up((y.w6_total + 1) / 2, 64) +
                align_up(y.act_total, 64) + align_up(y.grad_total, 64) +
                align_up((size_t)y.num_wg, 64) + align_up(y.dwp_total, 64) + align_up(y.dbp_total, 64) +
                64 + align_up((y.w16_total + 1) / 2, 64) + align_up(y.b16_total, 64) +
                align_up(y.mask_total * 2, 64) + 64 +   // + the fp16x3 weight/slab maxima
                align_up((size_t)kMaxLayers * kWmaxParts, 64) +   // + per-block max|W| partials
-               (train ? align_up((size_t)m.num_layers * y.num_wg * 64, 64) +      // per-sample shifts
-                            align_up((size_t)m.num_layers * y.num_wg * 8, 64) : 0);   // per-wave minima
+               (train ? align_up((size_t)m.num_layers * y.num_wg * tile / 2, 64) +   // per-sample shifts
+                            align_up((size_t)m.num_layers * y.num_wg * 8, 64) : 0);      // per-wave minima
+    return f;
+}
+
+// Either tile size (fused_plan runs 64 for k16 under LNERF_K16_W4, 128 otherwise).
+size_t fused_workspace_bytes(const lnerf_mlp& m, int rays, int S, bool train, int dw_grid) {
+    size_t f = workspace_floats(m, rays, S, train, dw_grid, kTileSamples);
+    if (S <= 64) {
+        const size_t f64 = workspace_floats(m, rays, S, train, dw_grid, 64);
+        f = f64 > f ? f64 : f;
+    }
     return f * sizeof(float);
 }
 
-void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws_base, int flags,
-                bool train, int dw_grid) {
+static void fused_plan_tile(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws_base, int flags,
+                            bool train, int dw_grid, int tile) {
     Layout y;
-    make_layout(y, m, b.rays, b.samples, train, dw_grid);
+    make_layout(y, m, b.rays, b.samples, train, dw_grid, tile);
+    p.tile = tile;
     p.L = m.num_layers;
     p.ht = y.ht;
     // The bf16/fp16 planes run on k16 (ReLU masks in HBM, any depth) unless the caller asks for the
@@ -1709,7 +1723,7 @@ void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws
     p.wmax_part = (int*)(base + off);
     off += align_up((size_t)kMaxLayers * kWmaxParts, 64);
     p.sexp = (signed char*)(base + off);
-    if (train) off += align_up((size_t)p.L * y.num_wg * 64, 64);   // L x num_wg x 128 x 2 bytes
+    if (train) off += align_up((size_t)p.L * y.num_wg * tile / 2, 64);   // L x num_wg x tile x 2 bytes
     p.epart = (int*)(base + off);
     if (train) off += align_up((size_t)p.L * y.num_wg * 8, 64);
 
@@ -1737,6 +1751,17 @@ void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws
     p.dw16 = p.k16 || p.k32;
     if (p.dw16)
         for (int l = 0; l < p.L; ++l) p.dw_phases[l] = 1;
+}
+
+void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws_base, int flags,
+                bool train, int dw_grid) {
+    fused_plan_tile(p, m, b, ws_base, flags, train, dw_grid, kTileSamples);
+    // k16 on 4-wave, 64-sample workgroups (two per CU) with LNERF_K16_W4, where whole rays fit 64
+    // samples and the ring fits 80 KiB (fp16x3 / plain bf16). Measured slower than the 8-wave
+    // workgroup at cfg3 (the second workgroup doubles the weight stream's LDS-DMA).
+    if (p.k16 && p.x6 != 3 && b.samples <= 64 && (flags & LNERF_K16_W4))
+        fused_plan_tile(p, m, b, ws_base, flags, train, dw_grid, 64);
+    p.head_fit = (flags & LNERF_HEAD_FIT) ? 1 : 0;
 }
 
 static void launch_pack(const FusedPlan& p, const float* ws, const float* bs, hipStream_t s) {
@@ -1936,7 +1961,8 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
     grad_reduce_kernel<<<(unsigned)((nred + 255) / 256), 256, 0, s>>>(ra);
     if (seed_loss) {
         if (out.d_dists) k_scale_by_scalar(out.d_dists, (size_t)p.R, p.loss_total, s);
-        if (out.d_target) k_scale_by_scalar(out.d_target, (size_t)p.rays * 3, p.loss_total, s);
+        if (out.d_target)
+            k_scale_by_scalar(out.d_target, (size_t)p.rays * (p.head_fit ? p.n[p.L - 1] : 3), p.loss_total, s);
         if (out.d_x) k_scale_by_scalar(out.d_x, (size_t)p.R * p.k[0], p.loss_total, s);
     }
     mark(5);

@@ -118,7 +118,9 @@ struct FusedPlan {
     int kt[kMaxLayers], nt[kMaxLayers]; // 32-wide tiles
     int w_k, w_n;
     int rays, S, R;                     // R = rays*S
-    int rays_per_wg;                    // whole rays per 128-sample workgroup tile
+    int tile;                           // samples per fused workgroup: 128, or 64 for k16 with
+                                        // 4-wave workgroups (two per CU; S <= 64, fp16x3 / bf16)
+    int rays_per_wg;                    // whole rays per workgroup tile
     int num_wg;                         // fused-kernel grid
     int blocks;                         // 32-sample slabs = num_wg * 4
     int input_mode, F;
@@ -152,6 +154,7 @@ struct FusedPlan {
     float* loss_total; // device scalar
     // k16 kernel (lnerf_k16.hip): 512-thread workgroups, two waves per SIMD, 16x16x32 MFMA
     int k16;                             // 1: the fused step runs k16 (pack16 + k16 kernel)
+    int head_fit;                        // 1: the mlp_fit head (LNERF_HEAD_FIT), k16 only
     int ht16;                            // 16-wide hidden output tiles (1/2/4/8/16)
     int ks16_f[kMaxLayers], ks16_b[kMaxLayers];   // k-steps (32 features) per pass
     int to16_f[kMaxLayers], to16_b[kMaxLayers];   // 16-wide output tiles per pass
@@ -172,7 +175,8 @@ struct FusedPlan {
     int* epart;                          // dw16: k1's per-wave min of exA + exG [L][num_wg * 8]
 };
 
-bool fused_supported(const lnerf_mlp& mlp, int rays, int S, int input_mode, const char** why);
+bool fused_supported(const lnerf_mlp& mlp, int rays, int S, int input_mode, const char** why,
+                     bool head_fit = false);
 // train = false sizes the forward-only (render) workspace: packed weights + loss partials.
 // dw_grid: the dW kernel's workgroup budget (0 = kDefaultDwGrid; LNERF_OPT_DW_GRID).
 size_t fused_workspace_bytes(const lnerf_mlp& mlp, int rays, int S, bool train = true, int dw_grid = 0);

@@ -35,13 +35,14 @@ typedef float fx4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
 typedef _Float16 hf8 __attribute__((ext_vector_type(8)));
 
-constexpr int kThreads = 512;
-constexpr int kWaves = 8;
-constexpr int kTile = comp::kTileSamples;     // 128 samples per workgroup
+// NW = waves per workgroup, 16 samples each: 8 (512 threads, a 128-sample tile, one workgroup
+// per CU) or 4 (256 threads, a 64-sample tile, two workgroups per CU: the two waves of a SIMD
+// then belong to different workgroups, so one's barrier waits, epilogues and compositing run
+// beside the other's MFMAs instead of in lockstep with them)
+constexpr int kWaves = 8;                     // the most waves per workgroup
 constexpr int kMaxChunks = 2 * kMaxLayers * 8 + 1;   // <= 2 passes x 8 k-steps per layer + 1 end
 constexpr int kMaxT = 16;                     // 16-feature tiles per 256-wide layer
 constexpr int kCompBytes = 2688 * 4;          // composite_tile's scratch (comp[0, 2688))
-constexpr int kLoaders = 8;                   // waves that issue the weight DMA (all)
 // timing experiments only (wrong results): drop the slab stores / the weight DMA after chunk 2
 #ifndef LNERF_K16_NOSTORE
 #define LNERF_K16_NOSTORE 0
@@ -60,15 +61,16 @@ constexpr int kLoaders = 8;                   // waves that issue the weight DMA
 //    of an early wave) in its middle, so the two waves of a SIMD run their chunk prologues half a
 //    chunk apart; the ring then needs 3 slots (the late waves still read the previous chunk
 //    while every wave reads the current one and the next one lands).
-template <int PL>
+//  * NW = 4 (two workgroups per CU, each within 80 KiB of LDS): KC = 1, two 32 KiB slots.
+template <int PL, int NW = 8>
 struct Ring {
-    static constexpr int KC = PL == 3 ? 1 : 2;
-    static constexpr bool stagger = PL == 3;
+    static constexpr int KC = (PL == 3 || NW == 4) ? 1 : 2;
+    static constexpr bool stagger = PL == 3 && NW == 8;
     static constexpr int slots = stagger ? 3 : 2;
     static constexpr int slot_bytes = KC * kMaxT * PL * 1024;
     static constexpr int off_comp = slots * slot_bytes;
     static constexpr int off_ray = off_comp + kCompBytes;
-    static constexpr int off_bias = off_ray + kTile * 4;
+    static constexpr int off_bias = off_ray + 16 * NW * 4;
     static constexpr int lds_bytes = off_bias + 3 * 256 * 4;   // + a 3-slot ring of layer biases
     static_assert(lds_bytes + 1024 <= 160 * 1024, "LDS budget (+1 KiB for the profiling build)");
     static_assert((KC * kMaxT - 1) * PL * 1024 < 65536, "ds_read offsets are 16-bit immediates");
@@ -111,6 +113,8 @@ struct K16Args {
     signed char* sexp;
     int rpad;          // slab positions (num_wg * 128)
     int* epart;        // training: per-wave min over samples of exA + exG, [l][num_wg * 8]
+    int head_fit;      // the mlp_fit head (comp::fit_tile) instead of the NeRF compositing
+    int nout;          // head outputs (the mlp_fit head's width)
 };
 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
@@ -165,19 +169,19 @@ __device__ __forceinline__ ChunkT chunk_at(const K16Args& a, int ci) {
 // workgroup, each wave instruction 1 KiB (lane-linear); the last wave also stages the biases a
 // first forward chunk carries (bias ring slot l % 3). Returns the instructions this wave issued
 // (what a later vmcnt must leave outstanding).
+template <int NW>
 __device__ __forceinline__ int dma_chunk(const K16Args& a, const ChunkT& c, unsigned char* dst,
                                          float* bias_ring) {
     const int tid = threadIdx.x, wave = wave_id();
     int n = 0;
     if (!c.src) return 0;
-    if (wave >= kLoaders) return 0;
-    for (int off = wave * 1024; off < c.bytes; off += kLoaders * 1024) {
+    for (int off = wave * 1024; off < c.bytes; off += NW * 1024) {
         const char* g = (const char*)c.src + off + (tid & 63) * 16;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                          (__attribute__((address_space(3))) void*)(dst + off), 16, 0, 0);
         ++n;
     }
-    if (c.bias >= 0 && wave == kLoaders - 1) {
+    if (c.bias >= 0 && wave == NW - 1) {
         const float* g = a.b16 + (size_t)c.bias * 256 + (tid & 63) * 4;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                          (__attribute__((address_space(3))) void*)(bias_ring + (c.bias % 3) * 256),
@@ -316,30 +320,30 @@ __device__ __forceinline__ void read_tile(unsigned base, bf8 (&w)[3]) {
 #ifndef LNERF_K16_SPREAD
 #define LNERF_K16_SPREAD 1
 #endif
-constexpr int kPiecesMax = 8;   // pieces per wave of a full chunk (64 KiB / 8 waves)
+constexpr int kPiecesMax = 8;   // pieces per wave of a full chunk (64 KiB / 8 waves, 32 KiB / 4)
 struct DmaJob {
     const char* src = nullptr;   // this lane's address of piece 0
     unsigned char* dst = nullptr;   // LDS address of this wave's piece 0
     int n = 0;                   // this wave's pieces of the chunk
 };
+template <int NW>
 __device__ __forceinline__ void dma_piece(const DmaJob& j, int p) {
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(j.src + p * (kLoaders * 1024)),
-                                     (__attribute__((address_space(3))) void*)(j.dst + p * (kLoaders * 1024)), 16, 0,
-                                     0);
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(j.src + p * (NW * 1024)),
+                                     (__attribute__((address_space(3))) void*)(j.dst + p * (NW * 1024)), 16, 0, 0);
 }
 // the pieces that land on output tile O: p with p * NTO / kPiecesMax == O (all on tile 0 when NTO == 1)
-template <int NTO, int O, int... P>
+template <int NTO, int O, int NW, int... P>
 __device__ __forceinline__ void dma_pieces_at(const DmaJob& j, std::integer_sequence<int, P...>) {
-    (((P * NTO) / kPiecesMax == O ? (P < j.n ? dma_piece(j, P) : void()) : void()), ...);
+    (((P * NTO) / kPiecesMax == O ? (P < j.n ? dma_piece<NW>(j, P) : void()) : void()), ...);
 }
 
 // Output tile O of one k-step: issue the reads of tile O + kDist, wait for tile O's (leaving
 // the younger ones in flight), the MFMAs (small terms first).
-template <int NTO, int PL, int O>
+template <int NTO, int PL, int NW, int O>
 __device__ __forceinline__ void tile_step(unsigned base, bf8 (&w)[kDist + 1][3], const bf8& bh,
                                           const bf8& bm, const bf8& bl, fx4 (&out)[kMaxT], const DmaJob& job) {
     if constexpr (O + kDist < NTO) read_tile<PL, O + kDist>(base, w[(O + kDist) % (kDist + 1)]);
-    if (job.n) dma_pieces_at<NTO, O>(job, std::make_integer_sequence<int, kPiecesMax>{});
+    if (job.n) dma_pieces_at<NTO, O, NW>(job, std::make_integer_sequence<int, kPiecesMax>{});
     constexpr int ahead = (NTO - 1 - O) < kDist ? (NTO - 1 - O) : kDist;
     bf8(&c)[3] = w[O % (kDist + 1)];
     lgkm_wait<ahead * (LNERF_K16_HALFLDS && PL == 2 ? 1 : PL)>(c);
@@ -363,11 +367,11 @@ __device__ __forceinline__ void tile_step(unsigned base, bf8 (&w)[kDist + 1][3],
 }
 
 // tiles B, B+1, ... of one k-step
-template <int NTO, int PL, int B, int... O>
+template <int NTO, int PL, int NW, int B, int... O>
 __device__ __forceinline__ void tile_steps(std::integer_sequence<int, O...>, unsigned base,
                                            bf8 (&w)[kDist + 1][3], const bf8& bh, const bf8& bm,
                                            const bf8& bl, fx4 (&out)[kMaxT], const DmaJob& job) {
-    (tile_step<NTO, PL, B + O>(base, w, bh, bm, bl, out, job), ...);
+    (tile_step<NTO, PL, NW, B + O>(base, w, bh, bm, bl, out, job), ...);
 }
 
 // The B operand planes of k-step s (the lane's 8 input features phi(s, g, 0..7) of its sample):
@@ -414,12 +418,12 @@ __device__ __forceinline__ void make_b(const fx4 (&in)[kMaxT], int s, int ex, bf
 // chunk ci + 1 and its last (LAST) meets the barrier that waits for it. (bh, bm, bl) hold k-step
 // s's B planes on entry and k-step s + 1's on exit. `slab` (nullable) receives the input tiles
 // (the A_{l-1} or G_l slab of this wave's half-block).
-template <int NTO, int PL>
+template <int NTO, int PL, int NW>
 __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk, bool last, int& ci,
                                          unsigned char* ring, float* bias_ring, const fx4 (&in)[kMaxT],
                                          fx4 (&out)[kMaxT], float* __restrict__ slab, int ex, bf8& bh,
                                          bf8& bm, bf8& bl, int& pending) {
-    using R = Ring<PL>;
+    using R = Ring<PL, NW>;
     const int lane = threadIdx.x & 63;
     const unsigned base = lds_addr(ring + (ci % R::slots) * R::slot_bytes) + kk * NTO * PL * 1024 + lane * 16;
     const bool st = slab && !LNERF_K16_NOSTORE;
@@ -437,12 +441,12 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
         if constexpr (spread) {
             const int wave = wave_id();
             const int woff = wave * 1024;
-            job.n = (c.src && woff < c.bytes) ? (c.bytes - woff + kLoaders * 1024 - 1) / (kLoaders * 1024) : 0;
+            job.n = (c.src && woff < c.bytes) ? (c.bytes - woff + NW * 1024 - 1) / (NW * 1024) : 0;
             job.src = (const char*)c.src + woff + lane * 16;
             job.dst = dst + woff;
             // the biases of a first forward chunk: one more piece from the last wave, now
             issued = job.n;
-            if (c.bias >= 0 && wave == kLoaders - 1) {
+            if (c.bias >= 0 && wave == NW - 1) {
                 const float* g = a.b16 + (size_t)c.bias * 256 + lane * 4;
                 __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                                  (__attribute__((address_space(3))) void*)(bias_ring + (c.bias % 3) * 256),
@@ -450,7 +454,7 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
                 ++issued;
             }
         } else {
-            issued = dma_chunk(a, c, dst, bias_ring);
+            issued = dma_chunk<NW>(a, c, dst, bias_ring);
         }
         asm volatile("" ::: "memory");   // the slab stores stay younger than the pieces
         pending = issued ? 0 : -1;
@@ -466,11 +470,11 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
     // the next prologue's critical path), second half, [spread: the slab stores, younger than
     // every piece], [early: barrier]
     constexpr int H = (NTO + 1) / 2;
-    tile_steps<NTO, PL, 0>(std::make_integer_sequence<int, H>{}, base, w, bh, bm, bl, out, job);
+    tile_steps<NTO, PL, NW, 0>(std::make_integer_sequence<int, H>{}, base, w, bh, bm, bl, out, job);
     if (late && last) dma_barrier(pending);
     bf8 nh = {}, nm = {}, nl = {};
     if (s + 1 < ks) make_b<PL>(in, s + 1 < 8 ? s + 1 : 0, ex, nh, nm, nl);
-    tile_steps<NTO, PL, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, bh, bm, bl, out, job);
+    tile_steps<NTO, PL, NW, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, bh, bm, bl, out, job);
     if (st && spread) {
         asm volatile("" ::: "memory");
         store_slab_step(slab + s * 1024, in[2 * s], in[2 * s + 1]);
@@ -483,11 +487,11 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
 }
 
 // One pass (a layer's forward or backward MMA) over its ks k-steps, Ring::KC k-steps per chunk.
-template <int NTO, int PL>
+template <int NTO, int PL, int NW>
 __device__ __forceinline__ void k16_pass(const K16Args& a, int ks, int& ci, unsigned char* ring,
                                          float* bias_ring, const fx4 (&in)[kMaxT], fx4 (&out)[kMaxT],
                                          float* __restrict__ slab, int ex = 0) {
-    constexpr int KC = Ring<PL>::KC;
+    constexpr int KC = Ring<PL, NW>::KC;
     bf8 bh = {}, bm = {}, bl = {};
     make_b<PL>(in, 0, ex, bh, bm, bl);
     int pending = 0;
@@ -496,20 +500,20 @@ __device__ __forceinline__ void k16_pass(const K16Args& a, int ks, int& ci, unsi
         if (s < ks) {
             const int kk = s % KC;
             const bool last = kk == KC - 1 || s + 1 == ks;
-            k16_step<NTO, PL>(a, ks, s, kk, last, ci, ring, bias_ring, in, out, slab, ex, bh, bm, bl, pending);
+            k16_step<NTO, PL, NW>(a, ks, s, kk, last, ci, ring, bias_ring, in, out, slab, ex, bh, bm, bl, pending);
         }
     }
 }
 
-template <int PL>
+template <int PL, int NW>
 __device__ __forceinline__ void k16_pass_n(const K16Args& a, int ks, int& ci, unsigned char* ring,
                                            float* bias_ring, int nto, const fx4 (&in)[kMaxT],
                                            fx4 (&out)[kMaxT], float* slab, int ex) {
-    if (nto <= 1) k16_pass<1, PL>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
-    else if (nto <= 2) k16_pass<2, PL>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
-    else if (nto <= 4) k16_pass<4, PL>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
-    else if (nto <= 8) k16_pass<8, PL>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
-    else k16_pass<16, PL>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
+    if (nto <= 1) k16_pass<1, PL, NW>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
+    else if (nto <= 2) k16_pass<2, PL, NW>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
+    else if (nto <= 4) k16_pass<4, PL, NW>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
+    else if (nto <= 8) k16_pass<8, PL, NW>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
+    else k16_pass<16, PL, NW>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
 }
 
 // The per-sample max|x| of a pass's input (lanes n, n + 16, n + 32, n + 48 hold sample n's
@@ -535,7 +539,7 @@ __device__ __forceinline__ int store_sexp(const K16Args& a, int l, int which, fl
     const int lane = threadIdx.x & 63;
     const int x = m > 0.0f ? shift_of(m) : -128;
     if (lane < 16) {
-        const int p = (blockIdx.x * kWaves + (threadIdx.x >> 6)) * 16 + lane;
+        const int p = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + lane;
         a.sexp[((size_t)l * a.rpad + p) * 2 + which] = (signed char)x;
     }
     return x;
@@ -568,7 +572,7 @@ __device__ __forceinline__ void store_emin(const K16Args& a, int l, int xa, int 
 #pragma unroll
     for (int d = 1; d < 16; d <<= 1) v = min(v, __shfl_xor(v, d));
     if ((threadIdx.x & 63) == 0)
-        a.epart[(size_t)l * gridDim.x * kWaves + blockIdx.x * kWaves + (threadIdx.x >> 6)] = v;
+        a.epart[((size_t)l * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)] = v;
 }
 
 // The layer's biases in the accumulator layout (fx4 = 4 consecutive features of a lane group),
@@ -600,9 +604,12 @@ __device__ __forceinline__ void zero_tiles(fx4 (&t)[kMaxT]) {
 
 // HT: 16-wide output tiles of every hidden layer (1/2/4/8/16); PL: operand planes (3 = bf16x6,
 // 2 = fp16x3, both fp32-class; 1 = plain bf16, inference).
-template <int HT, int PL>
-__global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
-    using R = Ring<PL>;
+// NW: waves per workgroup (8: 128-sample tiles, one workgroup per CU; 4: 64-sample tiles, two per
+// CU). Either way two waves share a SIMD and each gets at most 256 registers.
+template <int HT, int PL, int NW>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
+k16_fwd_bwd_kernel(K16Args a) {
+    using R = Ring<PL, NW>;
     __shared__ __attribute__((aligned(16))) unsigned char lds[R::lds_bytes];
     unsigned char* ring = lds;
     float* comp = (float*)(lds + R::off_comp);
@@ -619,7 +626,7 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
 #endif
     const int gs = wg * tile_samples + ls;             // global sample row (ray*S + j)
     const bool valid = (ls < tile_samples) && (gs < a.R);
-    const size_t blk = (size_t)wg * 4 + (wave >> 1);   // 32-sample slab block
+    const size_t blk = (size_t)wg * (NW / 2) + (wave >> 1);   // 32-sample slab block
     const int half = wave & 1;
     const bool st = a.want_grad != 0;
 #if LNERF_PROF
@@ -687,11 +694,11 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
     __syncthreads();   // the first DMA overwrites the scratch
 
     int ci = 0;   // chunk stream position (chunk_at)
-    dma_chunk(a, chunk_at(a, 0), ring, bias_ring);
+    dma_chunk<NW>(a, chunk_at(a, 0), ring, bias_ring);
     dma_barrier(0);
     PROF_ADD(kPfPE, t_start);
     // ReLU mask bits of this wave, per hidden layer: [L-1][lane] u64
-    unsigned long long* mask_w = a.mask_g + ((size_t)wg * (a.L - 1) * kWaves + wave) * 64 + lane;
+    unsigned long long* mask_w = a.mask_g + ((size_t)wg * (a.L - 1) * NW + wave) * 64 + lane;
 
     // ---- forward ----
     for (int l = 0; l < a.L; ++l) {
@@ -707,7 +714,7 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
         const int sh = unscale(l, ex);
         if (l < a.L - 1) {
             PROF_T(t_f);
-            k16_pass<HT, PL>(a, a.ks_f[l], ci, ring, bias_ring, act, out, slab, ex);
+            k16_pass<HT, PL, NW>(a, a.ks_f[l], ci, ring, bias_ring, act, out, slab, ex);
             PROF_ADD(kPfFwd, t_f);
             PROF_T(t_fe);
             // bias after the sum (nerf.py:98,125), ReLU (nerf.py:141-144) and its mask bits
@@ -725,10 +732,10 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
                     mb |= (pos ? 1ull : 0ull) << (4 * o + i);
                 }
             }
-            if (st) mask_w[(size_t)l * kWaves * 64] = mb;
+            if (st) mask_w[(size_t)l * NW * 64] = mb;
             PROF_ADD(kPfFwdEpi, t_fe);
         } else {
-            k16_pass<1, PL>(a, a.ks_f[l], ci, ring, bias_ring, act, out, slab, ex);
+            k16_pass<1, PL, NW>(a, a.ks_f[l], ci, ring, bias_ring, act, out, slab, ex);
             fx4 bv[kMaxT];
             bias_read<1>(std::make_integer_sequence<int, 1>{}, bl, bv);
             bias_wait<1>(std::make_integer_sequence<int, 1>{}, bv);
@@ -744,7 +751,8 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
     __syncthreads();
 
     // ---- rendering + loss + rendering reverse (one thread per sample, scans along rays) ----
-    comp::composite_tile(a, wg, comp, rayloss, st);
+    if (a.head_fit) comp::fit_tile(a, wg, comp, rayloss, st, a.nout);
+    else comp::composite_tile(a, wg, comp, rayloss, st);
     __syncthreads();
     if (tid == 0) {
         float lsum = 0.0f;
@@ -765,12 +773,12 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
         zero_tiles(out);
         float* slab = a.grad + a.grad_off[l] + blk * (size_t)(a.nt[l] * 1024) + half * 512;
         PROF_T(t_b);
-        const unsigned long long mb = mask_w[(size_t)(l - 1) * kWaves * 64];   // in flight over the pass
+        const unsigned long long mb = mask_w[(size_t)(l - 1) * NW * 64];   // in flight over the pass
         const float xm = sample_max(act);
         store_emin(a, l, exa.get(l), store_sexp(a, l, 1, xm));
         const int ex = shift_of(xm);
         const int sh = unscale(l, ex);
-        k16_pass<HT, PL>(a, a.ks_b[l], ci, ring, bias_ring, act, out, slab, ex);
+        k16_pass<HT, PL, NW>(a, a.ks_b[l], ci, ring, bias_ring, act, out, slab, ex);
         PROF_ADD(kPfBwd, t_b);
         PROF_T(t_be);
 #pragma unroll
@@ -791,7 +799,7 @@ __global__ void __launch_bounds__(kThreads, 1) k16_fwd_bwd_kernel(K16Args a) {
         store_emin(a, 0, exa.get(0), store_sexp(a, 0, 1, xm));
         const int ex = shift_of(xm);
         const int sh = unscale(0, ex);
-        k16_pass_n<PL>(a, a.ks_b[0], ci, ring, bias_ring, a.to_b[0], act, out, g0, ex);
+        k16_pass_n<PL, NW>(a, a.ks_b[0], ci, ring, bias_ring, a.to_b[0], act, out, g0, ex);
         if (valid) {
 #pragma unroll
             for (int o = 0; o < kMaxT; ++o)
@@ -911,7 +919,7 @@ __global__ void pack16_kernel(Pack16Args a) {
 // output byte; the bits come from two lanes' u64 mask words (lane g 16 + n holds features
 // 16 o + 4 g + i in bits 4 o + i).
 __global__ void k16_masks_kernel(const unsigned long long* __restrict__ mask_g, int L1, int R, int tile_samples,
-                                 unsigned char* __restrict__ out) {
+                                 int nw, unsigned char* __restrict__ out) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (size_t)L1 * R * 32) return;
     const int b = (int)(idx & 31);
@@ -919,7 +927,7 @@ __global__ void k16_masks_kernel(const unsigned long long* __restrict__ mask_g, 
     const int l = (int)(lr / R), r = (int)(lr % R);
     const int wg = r / tile_samples, ls = r % tile_samples, wave = ls >> 4, n = ls & 15;
     const int o = b >> 1, g0 = 2 * (b & 1);
-    const unsigned long long* w = mask_g + ((size_t)(wg * L1 + l) * kWaves + wave) * 64;
+    const unsigned long long* w = mask_g + ((size_t)(wg * L1 + l) * nw + wave) * 64;
     const unsigned lo = (unsigned)(w[g0 * 16 + n] >> (4 * o)) & 0xFu;
     const unsigned hi = (unsigned)(w[(g0 + 1) * 16 + n] >> (4 * o)) & 0xFu;
     out[idx] = (unsigned char)(lo | (hi << 4));
@@ -930,7 +938,8 @@ __global__ void k16_masks_kernel(const unsigned long long* __restrict__ mask_g, 
 void k16_masks_launch(const FusedPlan& p, unsigned char* out, hipStream_t s) {
     const size_t n = (size_t)(p.L - 1) * p.R * 32;
     if (n == 0) return;
-    k16_masks_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(p.mask_g, p.L - 1, p.R, p.rays_per_wg * p.S, out);
+    k16_masks_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(p.mask_g, p.L - 1, p.R, p.rays_per_wg * p.S,
+                                                                 p.tile / 16, out);
 }
 
 bool k16_supported(const FusedPlan& p) {
@@ -1011,15 +1020,17 @@ void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lner
     a.d_x = want_grad ? out.d_x : nullptr;
     a.seed = seed;
     a.want_grad = want_grad ? 1 : 0;
+    a.head_fit = p.head_fit;
+    a.nout = p.n[p.L - 1];
     a.planes = p.x6;
     a.wexp = p.wexp16;
     a.sexp = p.sexp;
-    a.rpad = p.num_wg * 128;
+    a.rpad = p.num_wg * p.tile;
     a.epart = p.epart;
     // the chunk stream: forward 0..L-1, backward L-1..1 (training), backward 0 (d_x); chunks of
     // KC k-steps (Ring: 2 for fp16x3 / bf16, 1 for bf16x6), the pack layout's consecutive k-steps
     {
-        const int KC = p.x6 == 3 ? 1 : 2;
+        const int KC = (p.x6 == 3 || p.tile == 64) ? 1 : 2;
         int ci = 0;
         auto add = [&](bool fwd, int l) {
             const int ks = fwd ? a.ks_f[l] : a.ks_b[l], to = fwd ? a.to_f[l] : a.to_b[l];
@@ -1037,13 +1048,17 @@ void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lner
     }
     static_assert(sizeof(K16Args) <= 4096, "kernel arguments");
 #ifdef LNERF_K16_ONLY_16_2   // compile-time experiments: one instantiation
-    k16_fwd_bwd_kernel<16, 2><<<p.num_wg, kThreads, 0, s>>>(a);
+    if (p.tile == 64) k16_fwd_bwd_kernel<16, 2, 4><<<p.num_wg, 256, 0, s>>>(a);
+    else k16_fwd_bwd_kernel<16, 2, 8><<<p.num_wg, 512, 0, s>>>(a);
     return;
 #endif
-#define LNERF_K16_LAUNCH(HT)                                                              \
-    if (p.x6 == 3) k16_fwd_bwd_kernel<HT, 3><<<p.num_wg, kThreads, 0, s>>>(a);            \
-    else if (p.x6 == 2) k16_fwd_bwd_kernel<HT, 2><<<p.num_wg, kThreads, 0, s>>>(a);       \
-    else k16_fwd_bwd_kernel<HT, 1><<<p.num_wg, kThreads, 0, s>>>(a);
+// bf16x6 (three planes) always runs the 8-wave workgroup (its ring does not fit two per CU)
+#define LNERF_K16_LAUNCH(HT)                                                                 \
+    if (p.x6 == 3) k16_fwd_bwd_kernel<HT, 3, 8><<<p.num_wg, 512, 0, s>>>(a);                 \
+    else if (p.tile == 64 && p.x6 == 2) k16_fwd_bwd_kernel<HT, 2, 4><<<p.num_wg, 256, 0, s>>>(a); \
+    else if (p.tile == 64) k16_fwd_bwd_kernel<HT, 1, 4><<<p.num_wg, 256, 0, s>>>(a);         \
+    else if (p.x6 == 2) k16_fwd_bwd_kernel<HT, 2, 8><<<p.num_wg, 512, 0, s>>>(a);            \
+    else k16_fwd_bwd_kernel<HT, 1, 8><<<p.num_wg, 512, 0, s>>>(a);
     switch (p.ht16) {
         case 1: LNERF_K16_LAUNCH(1) break;
         case 2: LNERF_K16_LAUNCH(2) break;
@@ -1060,7 +1075,7 @@ void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lner
         const char* names[] = {"pe", "fwd_pass", "fwd_epilogue", "barrier", "composite", "bwd_pass",
                                "bwd_epilogue", "tail", "total", "vmcnt_wait", "realtime_100MHz"};
         fprintf(stderr, "LNERF_PROF k16 per-wave cycles:");
-        for (int i = 0; i < kPfN; ++i) fprintf(stderr, " %s=%.0f", names[i], h[i] / ((double)p.num_wg * kWaves));
+        for (int i = 0; i < kPfN; ++i) fprintf(stderr, " %s=%.0f", names[i], h[i] / ((double)p.num_wg * (p.tile / 16)));
         fprintf(stderr, " clock_GHz=%.3f\n", h[kPfReal] ? (double)h[kPfTotal] / h[kPfReal] * 0.1 : 0.0);
         unsigned long long z[16] = {};
         (void)hipMemcpyToSymbol(HIP_SYMBOL(g_k16_prof), z, sizeof(z));

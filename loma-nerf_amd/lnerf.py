@@ -34,6 +34,8 @@ MFMA_F16X3 = 256  # fused path: fp16x3 split (22-bit products, fp32 accumulate; 
 MFMA_BF16X6 = 512  # fused path: bf16x6 split (fp32-accurate products)
 ONE_WAVE = 1024    # fused path: the one-wave-per-SIMD kernel pair instead of k16 + dw16 (A/B)
 K32 = 2048         # fused path: the 32-samples-per-wave 32x32 MFMA kernel instead of k16 (A/B)
+K16_W4 = 4096      # fused path: k16 on 4-wave 64-sample workgroups, two per CU (A/B)
+HEAD_FIT = 8192    # the mlp_fit head (sigmoid on every output, no compositing; samples = 1)
 
 OPT_DW_GRID = 1    # lnerf_ctx_set_option: dW workgroups per step (0 = default 512)
 
@@ -52,6 +54,7 @@ PATH_FUSED = 2
 PATH_K16 = 4
 PATH_DW16 = 8
 PATH_K32 = 16
+PATH_K16_W4 = 32
 
 
 class LnerfMLP(ctypes.Structure):
@@ -268,6 +271,25 @@ class Engine:
             raise RuntimeError(f"lnerf_train_step: {last_error()}")
         return StepResult(loss[0], acc_color, g, dws, dbs, d_dists, d_target, d_x)
 
+    def mlp_fit_step(self, mlp: LnerfMLP, ws, bs, x, target, *, seed=None, flags: int = 0, grads=None,
+                     outputs=None, want_grad: bool = True):
+        """fit_img.py's chunk step on the device (scripts/mlp_fit.py): the MLP on `x` (rows, k[0])
+        ENCODED rows, sigmoid on every output, loss = sum (sigmoid(z) - target)^2 over
+        (rows, n_out); with want_grad the reverse pass (grad_mlp_fit) into `grads`, seeded with
+        `seed` (fit_img.py:515 passes the previous chunk loss) or, seed=None, with this loss.
+        Returns (loss, outputs (rows, n_out), grads)."""
+        torch = self.torch
+        rows, nout = target.shape[0], mlp.n[mlp.num_layers - 1]
+        if outputs is None:
+            outputs = torch.empty(rows, nout, dtype=torch.float32, device=target.device)
+        if not want_grad:
+            loss, out = self.render(mlp, ws, bs, x, None, target, samples=1, input_mode=INPUT_ENCODED,
+                                    flags=flags | HEAD_FIT, acc=outputs)
+            return loss, out, None
+        r = self.train_step(mlp, ws, bs, x, None, target, samples=1, input_mode=INPUT_ENCODED, seed=seed,
+                            flags=flags | HEAD_FIT, grads=grads, acc_color=outputs)
+        return r.loss, outputs, r.grads
+
     def render(self, mlp: LnerfMLP, ws, bs, x, dists, target, *, samples: int,
                input_mode: int = INPUT_POINTS, num_freqs: int = 5, near: float = 2.0,
                far: float = 6.0, flags: int = 0, acc=None, loss=None):
@@ -317,6 +339,7 @@ class Engine:
             raise RuntimeError(f"lnerf_ctx_last_path: {last_error()}")
         return dict(generic=bool(v & PATH_GENERIC), fused=bool(v & PATH_FUSED),
                     k16=bool(v & PATH_K16), dw16=bool(v & PATH_DW16), k32=bool(v & PATH_K32),
+                    k16_w4=bool(v & PATH_K16_W4),
                     planes=(v >> 8) & 3)
 
     def relu_masks(self, L: int, R: int):

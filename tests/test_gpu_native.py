@@ -66,7 +66,8 @@ def compare(got, want, keys=("dW", "dB", "d_dists", "d_target"), tol=TOL):
         assert_close(k, got[k], want[k], **tol)
 
 
-FUSED = [0, 512]      # k16 + dw16: default fp16x3 split, lnerf.MFMA_BF16X6
+FUSED = [0, 512, 4096]   # k16 + dw16: default fp16x3 split, lnerf.MFMA_BF16X6, lnerf.K16_W4 (fp16x3
+                          # on 4-wave 64-sample workgroups, two per CU, instead of one 8-wave one)
 K32 = [2048, 2048 | 512]  # lnerf.K32 (32 samples per wave, 32x32 MFMA) + dw16: fp16x3, bf16x6
 ONE_WAVE = [64, 1024]  # one-wave pair: lnerf.MFMA_F32 (exact f32), lnerf.ONE_WAVE (bf16x6)
 
@@ -138,20 +139,23 @@ def test_fused_deep_mlp(engine, prec):
     if prec in FUSED + K32:
         check_fused(engine, w, flags=prec)
         k32 = bool(prec & lnerf.K32)
+        w4 = bool(prec & lnerf.K16_W4)
         assert engine.last_path() == dict(generic=False, fused=True, k16=not k32, dw16=True, k32=k32,
-                                          planes=3 if prec & lnerf.MFMA_BF16X6 else 2)
+                                          k16_w4=w4, planes=3 if prec & lnerf.MFMA_BF16X6 else 2)
         return
     got = run_native(engine, nerf_np.without_relu_ties(w) if prec != 128 else w,
                      flags=lnerf.FAST | prec)
     path = engine.last_path()
     if prec == 128:
         # plain bf16 operands (8 significant bits): a loose sanity bound, not the fp32 tolerance
-        assert path == dict(generic=False, fused=True, k16=True, dw16=True, k32=False, planes=1), path
+        assert path == dict(generic=False, fused=True, k16=True, dw16=True, k32=False, k16_w4=False,
+                            planes=1), path
         want = oracle_ref(w)
         assert abs(got["loss"] - want["loss"]) <= 2e-2 * abs(want["loss"]), (got["loss"], want["loss"])
         assert_close("dW", got["dW"], want["dW"], rtol=0.0, atol_scale=5e-2)
     else:
-        assert path == dict(generic=False, fused=True, k16=False, dw16=False, k32=False, planes=0), path
+        assert path == dict(generic=False, fused=True, k16=False, dw16=False, k32=False, k16_w4=False,
+                            planes=0), path
         compare(got, oracle_ref(nerf_np.without_relu_ties(w)), tol=TOL_F32)
 
 
@@ -162,12 +166,15 @@ def test_default_path_is_k16_dw16(engine):
     import lnerf
     w = nerf_np.make_workload("cfg3", rays=8)
     run_native(engine, w, per_ray=False)
-    assert engine.last_path() == dict(generic=False, fused=True, k16=True, dw16=True, k32=False, planes=2)
+    assert engine.last_path() == dict(generic=False, fused=True, k16=True, dw16=True, k32=False, k16_w4=False,
+                                      planes=2)
+    run_native(engine, w, per_ray=False, flags=lnerf.K16_W4)
+    assert engine.last_path()["k16"] and engine.last_path()["k16_w4"]
     run_native(engine, w, per_ray=False, flags=lnerf.MFMA_F16X3)
     assert engine.last_path()["planes"] == 2
     run_native(engine, w, per_ray=False, flags=lnerf.ONE_WAVE)
     assert engine.last_path() == dict(generic=False, fused=True, k16=False, dw16=False, k32=False,
-                                      planes=3)
+                                      k16_w4=False, planes=3)
     for bad in (lnerf.ONE_WAVE | lnerf.MFMA_F16X3, lnerf.MFMA_F16X3 | lnerf.MFMA_BF16X6,
                 lnerf.MFMA_BF16 | lnerf.MFMA_BF16X6):
         with pytest.raises(RuntimeError):

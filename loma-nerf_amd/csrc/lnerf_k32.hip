@@ -319,9 +319,44 @@ constexpr int read_ahead() { return NTO == 1 ? 1 : 3; }
 // caller points at a harmless address of this chunk's slot when no chunk of this pass follows),
 // wait for fragment F, its MFMAs into output tile F % NTO (small terms first). Every step keeps
 // kD younger reads in flight; the pass retires the last ones (k32_pass).
+// The chunk's vector-memory work, spread over its fragment steps (LNERF_K32_SPREAD) instead of
+// issued as one burst at the chunk's start, where a lone wave's matrix core would idle behind it
+// (timing knobs: the pieces cost 0.26 ms and the stores 0.24 ms of a 1.6 ms k1 as bursts): op i
+// of the 12 (this wave's <= 8 LDS-DMA pieces of the chunk two ahead, then the 4 slab stores of the
+// input tile, younger than every piece so the chunk barrier's vmcnt leaves them in flight) goes
+// between the first two (dependent) MFMAs of fragment step i NF / 12, where it issues while the
+// first one runs.
+#ifndef LNERF_K32_SPREAD
+#define LNERF_K32_SPREAD 1
+#endif
+struct VmJob {
+    const char* src = nullptr;      // this lane's address of piece 0
+    unsigned char* dst = nullptr;   // LDS address of this wave's piece 0
+    int n = 0;                      // this wave's pieces
+    float* slab = nullptr;          // the input tile's slab (nullptr: no stores)
+    const fx16* tile = nullptr;     // the input tile's registers
+};
+__device__ __forceinline__ void vm_op(const VmJob& j, int i) {
+    if (i < 8) {
+        if (i < j.n)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(j.src + i * (kWaves * 1024)),
+                                             (__attribute__((address_space(3))) void*)(j.dst + i * (kWaves * 1024)), 16,
+                                             0, 0);
+    } else if (j.slab) {
+        const int q = i - 8, lane = threadIdx.x & 63;
+        const fx16& v = *j.tile;
+        __builtin_nontemporal_store(fx4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]},
+                                    (fx4*)(j.slab + q * 256 + lane * 4));
+    }
+}
+template <int NF, int F, int... I>
+__device__ __forceinline__ void vm_ops_at(const VmJob& j, std::integer_sequence<int, I...>) {
+    (((I * NF) / 12 == F ? vm_op(j, I) : void()), ...);
+}
+
 template <int NTO, int PL, int F>
 __device__ __forceinline__ void frag_step(unsigned base, unsigned nbase, bf8 (&w)[4][3], const BOp& b,
-                                          fx16 (&out)[kMaxT]) {
+                                          fx16 (&out)[kMaxT], const VmJob& vj) {
     constexpr int NF = 2 * NTO, KD = read_ahead<NTO>();
     if constexpr (F + KD < NF) read_frag<PL, F + KD>(base, w[(F + KD) % (KD + 1)]);
     else read_frag<PL, F + KD - NF>(nbase, w[(F + KD) % (KD + 1)]);
@@ -330,6 +365,7 @@ __device__ __forceinline__ void frag_step(unsigned base, unsigned nbase, bf8 (&w
     fx16 acc = out[F % NTO];
     if constexpr (PL == 2) {
         acc = mfma32h(c[0], b.m, acc);   // w_hi x_lo, w_lo x_hi, then w_hi x_hi
+        if constexpr (LNERF_K32_SPREAD) vm_ops_at<NF, F>(vj, std::make_integer_sequence<int, 12>{});
         acc = mfma32h(c[1], b.h, acc);
         acc = mfma32h(c[0], b.h, acc);
     } else if constexpr (PL == 3) {
@@ -347,8 +383,8 @@ __device__ __forceinline__ void frag_step(unsigned base, unsigned nbase, bf8 (&w
 
 template <int NTO, int PL, int B, int... F>
 __device__ __forceinline__ void frag_steps(std::integer_sequence<int, F...>, unsigned base, unsigned nbase,
-                                           bf8 (&w)[4][3], const BOp& b, fx16 (&out)[kMaxT]) {
-    (frag_step<NTO, PL, B + F>(base, nbase, w, b, out), ...);
+                                           bf8 (&w)[4][3], const BOp& b, fx16 (&out)[kMaxT], const VmJob& vj) {
+    (frag_step<NTO, PL, B + F>(base, nbase, w, b, out, vj), ...);
 }
 
 // Slab tile store: input tile t of this wave's 32-sample block, [q][lane][4] = registers 4q..4q+3
@@ -380,9 +416,34 @@ __device__ __forceinline__ void k32_chunk(const K32Args& a, bool more, int& ci, 
     // DMA of chunk ci + 2 first (its table entry is a scalar load the compiler waits for with
     // lgkmcnt(0)), then the slab stores (younger than the pieces: the barrier's vmcnt leaves
     // them in flight)
-    const int issued = (LNERF_K32_NODMA && ci >= 2)
-                           ? 0
-                           : dma_chunk(a, chunk_at(a, ci + 2), ring + ((ci + 2) % kSlots) * SB, bias_ring);
+    constexpr bool spread = LNERF_K32_SPREAD && PL == 2;
+    const bool st = slab && !LNERF_K32_NOSTORE;
+    VmJob vj;
+    int issued;
+    {
+        const ChunkT c = (LNERF_K32_NODMA && ci >= 2) ? ChunkT{nullptr, 0, -1} : chunk_at(a, ci + 2);
+        unsigned char* dst = ring + ((ci + 2) % kSlots) * SB;
+        if constexpr (spread) {
+            // the pieces go out between the MFMAs below (vm_op); only a first forward chunk's
+            // biases are staged now, by the last wave
+            const int woff = wave_id() * 1024;
+            vj.n = (c.src && woff < c.bytes) ? (c.bytes - woff + kWaves * 1024 - 1) / (kWaves * 1024) : 0;
+            vj.src = (const char*)c.src + woff + lane * 16;
+            vj.dst = dst + woff;
+            vj.slab = st ? slab + T * 1024 : nullptr;
+            vj.tile = &in[T];
+            issued = vj.n;
+            if (c.bias >= 0 && wave_id() == kWaves - 1) {
+                const float* g = a.b16 + (size_t)c.bias * 256 + lane * 4;
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                                 (__attribute__((address_space(3))) void*)(bias_ring + (c.bias % 3) * 256),
+                                                 16, 0, 0);
+                ++issued;
+            }
+        } else {
+            issued = dma_chunk(a, c, dst, bias_ring);
+        }
+    }
     asm volatile("" ::: "memory");
     int pending = issued ? 0 : -1;
     if constexpr (T == 0) {
@@ -390,18 +451,18 @@ __device__ __forceinline__ void k32_chunk(const K32Args& a, bool more, int& ci, 
         if constexpr (KD >= 2) read_frag<PL, 1>(base, w[1]);
         if constexpr (KD >= 3) read_frag<PL, 2>(base, w[2]);
     }
-    if (slab && !LNERF_K32_NOSTORE) {
-        store_slab_tile(slab + T * 1024, in[T]);
+    if (st) {
+        if constexpr (!spread) store_slab_tile(slab + T * 1024, in[T]);
         if (pending >= 0) pending += 4;
     }
     // k-step 0: fragments 0..NTO-1; its k-step 1 split after step H
-    frag_steps<NTO, PL, 0>(std::make_integer_sequence<int, H + 1>{}, base, nbase, w, b, out);
+    frag_steps<NTO, PL, 0>(std::make_integer_sequence<int, H + 1>{}, base, nbase, w, b, out, vj);
     const BOp b1 = make_b<PL, 1>(in[T], ex);
-    frag_steps<NTO, PL, H + 1>(std::make_integer_sequence<int, NTO - H - 1>{}, base, nbase, w, b, out);
+    frag_steps<NTO, PL, H + 1>(std::make_integer_sequence<int, NTO - H - 1>{}, base, nbase, w, b, out, vj);
     // k-step 1: fragments NTO..2NTO-1; the next tile's k-step 0 split after step H
-    frag_steps<NTO, PL, NTO>(std::make_integer_sequence<int, H + 1>{}, base, nbase, w, b1, out);
+    frag_steps<NTO, PL, NTO>(std::make_integer_sequence<int, H + 1>{}, base, nbase, w, b1, out, vj);
     if constexpr (T + 1 < kMaxT) b = make_b<PL, 0>(in[T + 1], ex);
-    frag_steps<NTO, PL, NTO + H + 1>(std::make_integer_sequence<int, NTO - H - 1>{}, base, nbase, w, b1, out);
+    frag_steps<NTO, PL, NTO + H + 1>(std::make_integer_sequence<int, NTO - H - 1>{}, base, nbase, w, b1, out, vj);
     dma_barrier(pending);
     ++ci;
 }

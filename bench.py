@@ -70,6 +70,8 @@ def parse():
                     help="fwd+bwd only: skip the on-device Adam update (train_nerf.py:133-161) "
                          "that every timed step otherwise applies after the gradient exchange")
     ap.add_argument("--lr", type=float, default=5e-4, help="Adam learning rate (train_nerf.py)")
+    ap.add_argument("--no-render", action="store_true",
+                    help="skip the config-5 render record the default N=1 line carries")
     return ap.parse_args()
 
 
@@ -138,10 +140,12 @@ def cpu_baseline(args, cfg):
              "sample": f"{rn} rays x {b['S']} samples, OpenMP over rays, {tn:.1f}s"})
 
 
-def bench_render(args, world, rank, local, dist):
+def bench_render(args, world, rank, local, dist, steps=None, warmup=None):
     """Config 5: 800x800 frame, 128 samples/ray, MLP 33->256x7->4, forward only.
     The frame's 640 000 rays come from the device get_rays; each rank renders a contiguous share
-    (replicas, no collective in the timed region)."""
+    (replicas, no collective in the timed region). Returns rank 0's JSON record (None elsewhere)."""
+    steps = args.steps if steps is None else steps
+    warmup = args.warmup if warmup is None else warmup
     import numpy as np
     import torch
     import dp
@@ -169,14 +173,14 @@ def bench_render(args, world, rank, local, dist):
         eng.render(mlp, ws, bs, rays, None, target, samples=S, input_mode=lnerf.INPUT_RAYS,
                    num_freqs=F, flags=flags, acc=acc, loss=loss)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     torch.cuda.synchronize()
     if dist:
@@ -187,17 +191,18 @@ def bench_render(args, world, rank, local, dist):
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    ms = dt / args.steps * 1e3
+    ms = dt / steps * 1e3
     total = side * side * S
     fwd_flops = 2 * sum(k * n for k, n in shapes)
+    rec = None
     if rank == 0:
         mode = "f32" if args.mfma_f32 else "fp16x3" if args.x6 else "bf16"
         peak = PEAK_FP32_TFLOPS if args.mfma_f32 else PEAK_F16X3_TFLOPS if args.x6 else PEAK_BF16_TFLOPS
         ach = fwd_flops * N * S / (ms / 1e3) / 1e12
-        print(json.dumps({
+        rec = {
             "metric": "ray-samples/sec fwd (eval render), 800x800 frame x 128 samples",
             "value": total / (ms / 1e3), "unit": "ray-samples/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+            "steps": steps, "warmup": warmup, "ms_per_step": ms,
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
             "dtype": mode, "data": "synthetic (device get_rays of a look-at camera, random-init "
                                    "MLP seed 215)",
@@ -211,8 +216,9 @@ def bench_render(args, world, rank, local, dist):
                          "traffic": None,
                          "note": "rank-0 per-GPU rate: 2*sum(KN) FLOP/sample x its samples / "
                                  "step time (includes get_rays-free sampling + PE + compositing)"},
-        }), flush=True)
+        }
     eng.close()
+    return rec
 
 
 def main():
@@ -234,7 +240,9 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     if args.render:
-        bench_render(args, world, rank, local, dist)
+        rec = bench_render(args, world, rank, local, dist)
+        if rec:
+            print(json.dumps(rec), flush=True)
         if dist:
             dist.destroy_process_group()
         return
@@ -396,6 +404,14 @@ def main():
                                     "achieved_gbs": slab_b * N * S / (kt["dw"] / 1e3) / 1e9,
                                     "peak_gbs": PEAK_HBM_GBS,
                                     "frac": slab_b * N * S / (kt["dw"] / 1e3) / 1e9 / PEAK_HBM_GBS}
+        if world == 1 and not (args.no_render or args.generic or args.strong or args.rays):
+            # config 5 (forward-only 800x800x128 bf16 eval render) on the same GPU, timed the same
+            # way (its own warmup, barrier + synchronize brackets), so that it has a driver record
+            eng.close()
+            r5 = bench_render(argparse.Namespace(mfma_f32=False, x6=False), 1, 0, local, None,
+                              steps=5, warmup=2)
+            out["config5_render"] = {k: r5[k] for k in ("metric", "value", "unit", "ms_per_step", "steps",
+                                                         "warmup", "dtype", "config", "roofline")}
         if world == 1 and not args.no_cpu_baseline:
             c1, cn = cpu_baseline(args, args.config)
             out["cpu_baseline"] = c1

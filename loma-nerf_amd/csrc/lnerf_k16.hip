@@ -50,6 +50,9 @@ constexpr int kCompBytes = 2688 * 4;          // composite_tile's scratch (comp[
 #ifndef LNERF_K16_NODMA
 #define LNERF_K16_NODMA 0
 #endif
+#ifndef LNERF_K16_NOBAR
+#define LNERF_K16_NOBAR 0
+#endif
 
 // The weight stream of a PL-plane kernel. A chunk is KC k-steps (32 input features each) x every
 // output tile x PL planes, delivered by LDS-DMA into one slot of a ring, one workgroup barrier per
@@ -215,7 +218,9 @@ __device__ __forceinline__ void dma_barrier(int pending) {
     else if (pending == 4) vm_wait<4>();
     else if (pending > 0) vm_wait_n(pending, std::make_integer_sequence<int, 64>{});
     PROF_ADD(kPfVm, t0);
+#if !LNERF_K16_NOBAR   // timing experiment only (wrong results): no chunk barrier
     __builtin_amdgcn_s_barrier();
+#endif
     asm volatile("" ::: "memory");
     PROF_ADD(kPfBar, t0);
 }

@@ -3,7 +3,7 @@ set -u
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 for lib in "$@"; do
-  LNERF_LIB=$lib timeout -k 10 120 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/ab.log 2>&1 || { echo "$lib failed"; tail -5 gpurun_out/ab.log; exit 1; }
+  LNERF_LIB=$lib timeout -k 10 120 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-render ${BENCH_ARGS:-} > gpurun_out/ab.log 2>&1 || { echo "$lib failed"; tail -5 gpurun_out/ab.log; exit 1; }
   python - "$lib" <<'PY'
 import json, sys
 line = [l for l in open("gpurun_out/ab.log") if l.startswith("{")][-1]

@@ -14,7 +14,7 @@ i=0
 for P in "$P1" "$P2" "$P3"; do
   i=$((i+1))
   timeout -s KILL 150 rocprofv3 --pmc $P --output-format csv -d "$OUT/p$i" -o run -- \
-    python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline "$@" > "$OUT/p$i.log" 2>&1 \
+    python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-render "$@" > "$OUT/p$i.log" 2>&1 \
     || { echo "sq pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
   echo "sq pass $i ok"
 done

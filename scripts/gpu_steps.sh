@@ -20,7 +20,7 @@ for step in "$@"; do
     k32)
       timeout -k 10 300 python -u -m pytest tests/test_gpu_native.py -m gpu -x -q -p no:cacheprovider \
         --timeout 120 --timeout-method thread -k "2048 or 2560" > gpurun_out/k32tests.log 2>&1 &&
-      timeout -k 10 300 python bench.py --k32 --no-cpu-baseline > gpurun_out/k32bench.log 2>&1
+      timeout -k 10 300 python bench.py --k32 --no-cpu-baseline --no-render > gpurun_out/k32bench.log 2>&1
       rc=$?; tail -3 gpurun_out/k32tests.log; tail -1 gpurun_out/k32bench.log | cut -c1-900 ;;
     k32trace)
       mkdir -p gpurun_out/prof
@@ -52,16 +52,16 @@ for step in "$@"; do
       mkdir -p gpurun_out/prof
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
         -d "$R/gpurun_out/prof/trace" -o run -- python3 "$R/bench.py" --steps 10 --warmup 3 \
-        --no-cpu-baseline > "$R/gpurun_out/prof/trace.log" 2>&1)
+        --no-cpu-baseline --no-render > "$R/gpurun_out/prof/trace.log" 2>&1)
       rc=$? ;;
     pmc)
       mkdir -p gpurun_out/prof
       (cd /tmp && timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv \
         -d "$R/gpurun_out/prof/fetch" -o run -- python3 "$R/bench.py" --steps 10 --warmup 3 \
-        --no-cpu-baseline > "$R/gpurun_out/prof/fetch.log" 2>&1) &&
+        --no-cpu-baseline --no-render > "$R/gpurun_out/prof/fetch.log" 2>&1) &&
       (cd /tmp && timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv \
         -d "$R/gpurun_out/prof/write" -o run -- python3 "$R/bench.py" --steps 10 --warmup 3 \
-        --no-cpu-baseline > "$R/gpurun_out/prof/write.log" 2>&1)
+        --no-cpu-baseline --no-render > "$R/gpurun_out/prof/write.log" 2>&1)
       rc=$? ;;
     sq)
       bash scripts/gpu_sq.sh

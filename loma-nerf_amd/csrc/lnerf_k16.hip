@@ -53,6 +53,10 @@ constexpr int kCompBytes = 2688 * 4;          // composite_tile's scratch (comp[
 #ifndef LNERF_K16_NOBAR
 #define LNERF_K16_NOBAR 0
 #endif
+// full hidden passes get compile-time step bounds and test-free DMA issue (A/B: 0 = generic only)
+#ifndef LNERF_K16_FULLDMA
+#define LNERF_K16_FULLDMA 1
+#endif
 
 // The weight stream of a PL-plane kernel. A chunk is KC k-steps (32 input features each) x every
 // output tile x PL planes, delivered by LDS-DMA into one slot of a ring, one workgroup barrier per
@@ -327,28 +331,32 @@ __device__ __forceinline__ void read_tile(unsigned base, bf8 (&w)[3]) {
 #endif
 constexpr int kPiecesMax = 8;   // pieces per wave of a full chunk (64 KiB / 8 waves, 32 KiB / 4)
 struct DmaJob {
-    const char* src = nullptr;   // this lane's address of piece 0
+    const char* src = nullptr;   // the wave's (uniform) address of piece 0
     unsigned char* dst = nullptr;   // LDS address of this wave's piece 0
     int n = 0;                   // this wave's pieces of the chunk
 };
 template <int NW>
 __device__ __forceinline__ void dma_piece(const DmaJob& j, int p) {
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(j.src + p * (NW * 1024)),
-                                     (__attribute__((address_space(3))) void*)(j.dst + p * (NW * 1024)), 16, 0, 0);
+    const int lane = threadIdx.x & 63;
+    __builtin_amdgcn_global_load_lds(
+        (const __attribute__((address_space(1))) void*)(j.src + p * (NW * 1024) + lane * 16),
+        (__attribute__((address_space(3))) void*)(j.dst + p * (NW * 1024)), 16, 0, 0);
 }
-// the pieces that land on output tile O: p with p * NTO / kPiecesMax == O (all on tile 0 when NTO == 1)
-template <int NTO, int O, int NW, int... P>
+// the pieces that land on output tile O: p with p * NTO / kPiecesMax == O (all on tile 0 when NTO == 1);
+// FULL: the chunk is known to be whole (every wave issues kPiecesMax pieces, no per-piece test)
+template <int NTO, int O, int NW, bool FULL, int... P>
 __device__ __forceinline__ void dma_pieces_at(const DmaJob& j, std::integer_sequence<int, P...>) {
-    (((P * NTO) / kPiecesMax == O ? (P < j.n ? dma_piece<NW>(j, P) : void()) : void()), ...);
+    (((P * NTO) / kPiecesMax == O ? ((FULL || P < j.n) ? dma_piece<NW>(j, P) : void()) : void()), ...);
 }
 
 // Output tile O of one k-step: issue the reads of tile O + kDist, wait for tile O's (leaving
 // the younger ones in flight), the MFMAs (small terms first).
-template <int NTO, int PL, int NW, int O>
+template <int NTO, int PL, int NW, bool FD, int O>
 __device__ __forceinline__ void tile_step(unsigned base, bf8 (&w)[kDist + 1][3], const bf8& bh,
                                           const bf8& bm, const bf8& bl, fx4 (&out)[kMaxT], const DmaJob& job) {
     if constexpr (O + kDist < NTO) read_tile<PL, O + kDist>(base, w[(O + kDist) % (kDist + 1)]);
-    if (job.n) dma_pieces_at<NTO, O, NW>(job, std::make_integer_sequence<int, kPiecesMax>{});
+    if constexpr (FD) dma_pieces_at<NTO, O, NW, true>(job, std::make_integer_sequence<int, kPiecesMax>{});
+    else if (job.n) dma_pieces_at<NTO, O, NW, false>(job, std::make_integer_sequence<int, kPiecesMax>{});
     constexpr int ahead = (NTO - 1 - O) < kDist ? (NTO - 1 - O) : kDist;
     bf8(&c)[3] = w[O % (kDist + 1)];
     lgkm_wait<ahead * (LNERF_K16_HALFLDS && PL == 2 ? 1 : PL)>(c);
@@ -372,11 +380,11 @@ __device__ __forceinline__ void tile_step(unsigned base, bf8 (&w)[kDist + 1][3],
 }
 
 // tiles B, B+1, ... of one k-step
-template <int NTO, int PL, int NW, int B, int... O>
+template <int NTO, int PL, int NW, bool FD, int B, int... O>
 __device__ __forceinline__ void tile_steps(std::integer_sequence<int, O...>, unsigned base,
                                            bf8 (&w)[kDist + 1][3], const bf8& bh, const bf8& bm,
                                            const bf8& bl, fx4 (&out)[kMaxT], const DmaJob& job) {
-    (tile_step<NTO, PL, NW, B + O>(base, w, bh, bm, bl, out, job), ...);
+    (tile_step<NTO, PL, NW, FD, B + O>(base, w, bh, bm, bl, out, job), ...);
 }
 
 // The B operand planes of k-step s (the lane's 8 input features phi(s, g, 0..7) of its sample):
@@ -423,7 +431,9 @@ __device__ __forceinline__ void make_b(const fx4 (&in)[kMaxT], int s, int ex, bf
 // chunk ci + 1 and its last (LAST) meets the barrier that waits for it. (bh, bm, bl) hold k-step
 // s's B planes on entry and k-step s + 1's on exit. `slab` (nullable) receives the input tiles
 // (the A_{l-1} or G_l slab of this wave's half-block).
-template <int NTO, int PL, int NW>
+// FD: this k-step issues the DMA of a chunk known to be whole (the next chunk of the same full
+// pass): kPiecesMax pieces per wave with no per-piece test and no byte arithmetic.
+template <int NTO, int PL, int NW, bool FD = false>
 __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk, bool last, int& ci,
                                          unsigned char* ring, float* bias_ring, const fx4 (&in)[kMaxT],
                                          fx4 (&out)[kMaxT], float* __restrict__ slab, int ex, bf8& bh,
@@ -446,8 +456,9 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
         if constexpr (spread) {
             const int wave = wave_id();
             const int woff = wave * 1024;
-            job.n = (c.src && woff < c.bytes) ? (c.bytes - woff + NW * 1024 - 1) / (NW * 1024) : 0;
-            job.src = (const char*)c.src + woff + lane * 16;
+            job.n = FD ? kPiecesMax
+                       : (c.src && woff < c.bytes) ? (c.bytes - woff + NW * 1024 - 1) / (NW * 1024) : 0;
+            job.src = (const char*)c.src + woff;
             job.dst = dst + woff;
             // the biases of a first forward chunk: one more piece from the last wave, now
             issued = job.n;
@@ -475,11 +486,11 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
     // the next prologue's critical path), second half, [spread: the slab stores, younger than
     // every piece], [early: barrier]
     constexpr int H = (NTO + 1) / 2;
-    tile_steps<NTO, PL, NW, 0>(std::make_integer_sequence<int, H>{}, base, w, bh, bm, bl, out, job);
+    tile_steps<NTO, PL, NW, FD, 0>(std::make_integer_sequence<int, H>{}, base, w, bh, bm, bl, out, job);
     if (late && last) dma_barrier(pending);
     bf8 nh = {}, nm = {}, nl = {};
     if (s + 1 < ks) make_b<PL>(in, s + 1 < 8 ? s + 1 : 0, ex, nh, nm, nl);
-    tile_steps<NTO, PL, NW, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, bh, bm, bl, out, job);
+    tile_steps<NTO, PL, NW, FD, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, bh, bm, bl, out, job);
     if (st && spread) {
         asm volatile("" ::: "memory");
         store_slab_step(slab + s * 1024, in[2 * s], in[2 * s + 1]);
@@ -491,23 +502,55 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
     bl = nl;
 }
 
+// One k-step S of a pass. FULL: the pass has all 8 k-steps (a 256-wide input), so the step
+// bounds are compile-time and, where the chunk after this one belongs to the same pass and is
+// whole (KC NTO PL KiB = kPiecesMax pieces per wave), its DMA is issued without per-piece tests.
+template <int NTO, int PL, int NW, bool FULL, int S>
+__device__ __forceinline__ void k16_pass_step(const K16Args& a, int ks, int& ci, unsigned char* ring,
+                                              float* bias_ring, const fx4 (&in)[kMaxT], fx4 (&out)[kMaxT],
+                                              float* __restrict__ slab, int ex, bf8& bh, bf8& bm, bf8& bl,
+                                              int& pending) {
+    constexpr int KC = Ring<PL, NW>::KC;
+    if (FULL || S < ks) {
+        constexpr int kk = S % KC;
+        const bool last = kk == KC - 1 || (FULL ? S == 7 : S + 1 == ks);
+        constexpr bool fd = LNERF_K16_FULLDMA && FULL && kk == 0 && S / KC + 1 < 8 / KC &&
+                            KC * NTO * PL == kPiecesMax * NW && LNERF_K16_SPREAD && !Ring<PL, NW>::stagger;
+        k16_step<NTO, PL, NW, fd>(a, FULL ? 8 : ks, S, kk, last, ci, ring, bias_ring, in, out, slab, ex, bh, bm,
+                                  bl, pending);
+    }
+}
+template <int NTO, int PL, int NW, bool FULL, int... S>
+__device__ __forceinline__ void k16_pass_steps(std::integer_sequence<int, S...>, const K16Args& a, int ks, int& ci,
+                                               unsigned char* ring, float* bias_ring, const fx4 (&in)[kMaxT],
+                                               fx4 (&out)[kMaxT], float* __restrict__ slab, int ex, bf8& bh,
+                                               bf8& bm, bf8& bl, int& pending) {
+    (k16_pass_step<NTO, PL, NW, FULL, S>(a, ks, ci, ring, bias_ring, in, out, slab, ex, bh, bm, bl, pending), ...);
+}
+
 // One pass (a layer's forward or backward MMA) over its ks k-steps, Ring::KC k-steps per chunk.
-template <int NTO, int PL, int NW>
+template <int NTO, int PL, int NW, bool FULL = false>
 __device__ __forceinline__ void k16_pass(const K16Args& a, int ks, int& ci, unsigned char* ring,
                                          float* bias_ring, const fx4 (&in)[kMaxT], fx4 (&out)[kMaxT],
                                          float* __restrict__ slab, int ex = 0) {
-    constexpr int KC = Ring<PL, NW>::KC;
     bf8 bh = {}, bm = {}, bl = {};
     make_b<PL>(in, 0, ex, bh, bm, bl);
     int pending = 0;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-        if (s < ks) {
-            const int kk = s % KC;
-            const bool last = kk == KC - 1 || s + 1 == ks;
-            k16_step<NTO, PL, NW>(a, ks, s, kk, last, ci, ring, bias_ring, in, out, slab, ex, bh, bm, bl, pending);
+    k16_pass_steps<NTO, PL, NW, FULL>(std::make_integer_sequence<int, 8>{}, a, ks, ci, ring, bias_ring, in, out, slab,
+                                      ex, bh, bm, bl, pending);
+}
+// a hidden layer's pass: the FULL instantiation for 256-wide inputs (every hidden layer of cfg3)
+template <int HT, int PL, int NW>
+__device__ __forceinline__ void k16_hidden_pass(const K16Args& a, int ks, int& ci, unsigned char* ring,
+                                                float* bias_ring, const fx4 (&in)[kMaxT], fx4 (&out)[kMaxT],
+                                                float* __restrict__ slab, int ex) {
+    if constexpr (LNERF_K16_FULLDMA && HT == 16) {
+        if (ks == 8) {
+            k16_pass<HT, PL, NW, true>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
+            return;
         }
     }
+    k16_pass<HT, PL, NW, false>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
 }
 
 template <int PL, int NW>
@@ -719,7 +762,7 @@ k16_fwd_bwd_kernel(K16Args a) {
         const int sh = unscale(l, ex);
         if (l < a.L - 1) {
             PROF_T(t_f);
-            k16_pass<HT, PL, NW>(a, a.ks_f[l], ci, ring, bias_ring, act, out, slab, ex);
+            k16_hidden_pass<HT, PL, NW>(a, a.ks_f[l], ci, ring, bias_ring, act, out, slab, ex);
             PROF_ADD(kPfFwd, t_f);
             PROF_T(t_fe);
             // bias after the sum (nerf.py:98,125), ReLU (nerf.py:141-144) and its mask bits
@@ -783,7 +826,7 @@ k16_fwd_bwd_kernel(K16Args a) {
         store_emin(a, l, exa.get(l), store_sexp(a, l, 1, xm));
         const int ex = shift_of(xm);
         const int sh = unscale(l, ex);
-        k16_pass<HT, PL, NW>(a, a.ks_b[l], ci, ring, bias_ring, act, out, slab, ex);
+        k16_hidden_pass<HT, PL, NW>(a, a.ks_b[l], ci, ring, bias_ring, act, out, slab, ex);
         PROF_ADD(kPfBwd, t_b);
         PROF_T(t_be);
 #pragma unroll

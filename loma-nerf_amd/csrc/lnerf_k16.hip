@@ -645,6 +645,18 @@ __device__ __forceinline__ void bias_wait(std::integer_sequence<int, O...>, fx4 
     (lgkm_wait4<NT - 1 - O>(b[O]), ...);
 }
 
+// ReLU and its mask bit in one short dependency chain (nerf.py:141-144): r = v > 0 ? v : 0 (NaN
+// and -0 give +0) and bits = 2 bits + (v > 0), through VCC. Written out because the compiler
+// otherwise keeps all 64 compare masks of a layer live in SGPRs and spills them to VGPR lanes.
+__device__ __forceinline__ float relu_bit(float v, unsigned& bits) {
+    float r;
+    asm("v_cmp_lt_f32_e32 vcc, 0, %2\n\t"
+        "v_cndmask_b32_e32 %0, 0, %2, vcc\n\t"
+        "v_addc_co_u32_e32 %1, vcc, %1, %1, vcc"
+        : "=&v"(r), "+v"(bits) : "v"(v) : "vcc");
+    return r;
+}
+
 __device__ __forceinline__ void zero_tiles(fx4 (&t)[kMaxT]) {
 #pragma unroll
     for (int o = 0; o < kMaxT; ++o) t[o] = fx4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -769,17 +781,17 @@ k16_fwd_bwd_kernel(K16Args a) {
             fx4 bv[kMaxT];
             bias_read<HT>(std::make_integer_sequence<int, HT>{}, bl, bv);
             bias_wait<HT>(std::make_integer_sequence<int, HT>{}, bv);
-            unsigned long long mb = 0ull;
+            // values in descending bit order (feature 4o + i ends in bit 4o + i of lo / hi)
+            unsigned mlo = 0u, mhi = 0u;
 #pragma unroll
-            for (int o = 0; o < HT; ++o) {
+            for (int o = HT - 1; o >= 0; --o) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
+                for (int i = 3; i >= 0; --i) {
                     const float v = (PL >= 2 ? __builtin_ldexpf(out[o][i], sh) : out[o][i]) + bv[o][i];
-                    const bool pos = v > 0.0f;
-                    act[o][i] = pos ? v : 0.0f;
-                    mb |= (pos ? 1ull : 0ull) << (4 * o + i);
+                    act[o][i] = relu_bit(v, o >= 8 ? mhi : mlo);
                 }
             }
+            const unsigned long long mb = ((unsigned long long)mhi << 32) | mlo;
             if (st) mask_w[(size_t)l * NW * 64] = mb;
             PROF_ADD(kPfFwdEpi, t_fe);
         } else {
@@ -829,12 +841,16 @@ k16_fwd_bwd_kernel(K16Args a) {
         k16_hidden_pass<HT, PL, NW>(a, a.ks_b[l], ci, ring, bias_ring, act, out, slab, ex);
         PROF_ADD(kPfBwd, t_b);
         PROF_T(t_be);
+        // the forward's decision as an all-ones / zero lane mask (v_bfe_i32), one AND per value
+        const int mlo = (int)(unsigned)mb, mhi = (int)(unsigned)(mb >> 32);
 #pragma unroll
         for (int o = 0; o < HT; ++o)
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                act[o][i] = ((mb >> (4 * o + i)) & 1ull) ? (PL >= 2 ? __builtin_ldexpf(out[o][i], sh) : out[o][i])
-                                                         : 0.0f;
+            for (int i = 0; i < 4; ++i) {
+                const int keep = __builtin_amdgcn_sbfe(o >= 8 ? mhi : mlo, (4 * o + i) & 31, 1);
+                const float g = PL >= 2 ? __builtin_ldexpf(out[o][i], sh) : out[o][i];
+                act[o][i] = __int_as_float(__float_as_int(g) & keep);
+            }
         PROF_ADD(kPfBwdEpi, t_be);
     }
     PROF_T(t_t);

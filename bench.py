@@ -313,6 +313,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    t_host = time.perf_counter() - t0   # host enqueue time of the K steps (no sync inside)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -361,6 +362,7 @@ def main():
                        "input": ("rays: sampling, dists and positional encoding on the GPU"
                                  if args.input == "rays" else "points: sampled on the host")},
             "step_tflops": step_flops / (ms / 1e3) / 1e12,
+            "host_enqueue_ms_per_step": t_host / args.steps * 1e3,
         }
         if kt:
             fus_ms = kt["fused"]

@@ -37,6 +37,10 @@ typedef _Float16 hf4 __attribute__((ext_vector_type(4)));
 #ifndef LNERF_DW16_NOLOAD
 #define LNERF_DW16_NOLOAD 0
 #endif
+// half-blocks of slab loads in flight per thread (3: default; 2: 17 fewer registers)
+#ifndef LNERF_DW16_DEPTH
+#define LNERF_DW16_DEPTH 3
+#endif
 
 constexpr int kThreads = 512;
 constexpr int kRows = 512;                  // A rows [0, 256) and G rows [256, 512) of the image
@@ -346,6 +350,39 @@ __device__ __forceinline__ void hb_loop3(const float* A, const float* G, const u
     if (hb + 1 < hb1) hb_step3<PL, TI, TJ, ACTIVE, FULL, 1>(A, G, se, kt, nt, m, hb + 1, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
 }
 
+// Two half-blocks in flight (LNERF_DW16_DEPTH = 2): the same rotation over two register sets --
+// entering hb, set I held hb (split last step, free: it receives hb + 2), set I ^ 1 holds hb + 1
+// (split now). 17 fewer registers than the 3-deep rotation.
+template <int PL, int TI, int TJ, bool ACTIVE, bool FULL, int I>
+__device__ __forceinline__ void hb_step2(const float* A, const float* G, const unsigned short* se, int kt, int nt,
+                                         const RowMap& m, int hb, int hb0, int hb1, int a0, int g0,
+                                         fx16 (&acc)[TI][TJ], Loads& L0, Loads& L1, fx4 (&dbs)[2],
+                                         unsigned char* lds, int E) {
+    constexpr int kIB = image_bytes<PL>();
+    Loads& fr = I == 0 ? L0 : L1;
+    const Loads& nx = I == 0 ? L1 : L0;
+    issue_loads(A, G, se, kt, nt, m, hb + 2, hb1, fr);
+    if (hb + 1 < hb1) {
+        dbs[0] += nx.v[2];
+        dbs[1] += nx.v[3];
+    }
+    const int cur = (hb - hb0) & 1;
+    block_mma<PL, TI, TJ, ACTIVE, FULL>(lds + cur * kIB, a0, g0, acc, nx, lds + (cur ^ 1) * kIB, m, E);
+    __syncthreads();
+}
+
+template <int PL, int TI, int TJ, bool ACTIVE, bool FULL>
+__device__ __forceinline__ void hb_loop2(const float* A, const float* G, const unsigned short* se, int kt, int nt,
+                                         const RowMap& m, int hb0, int hb1, int a0, int g0, fx16 (&acc)[TI][TJ],
+                                         Loads& L0, Loads& L1, fx4 (&dbs)[2], unsigned char* lds, int E) {
+    int hb = hb0;
+    for (; hb + 2 <= hb1; hb += 2) {
+        hb_step2<PL, TI, TJ, ACTIVE, FULL, 0>(A, G, se, kt, nt, m, hb, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E);
+        hb_step2<PL, TI, TJ, ACTIVE, FULL, 1>(A, G, se, kt, nt, m, hb + 1, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E);
+    }
+    if (hb < hb1) hb_step2<PL, TI, TJ, ACTIVE, FULL, 0>(A, G, se, kt, nt, m, hb, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E);
+}
+
 // One split of layer l with TI x TJ tile blocks per wave (the layer's ceil(KT/TI) x ceil(NT/TJ)
 // blocks on waves 0.., at most 8).
 template <int PL, int TI, int TJ>
@@ -376,6 +413,21 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
     const unsigned short* se = a.sexp + (size_t)l * a.rpad;
     const int E = a.eshift[l];
     const bool full = KT == 8 && NT == 8;
+#if LNERF_DW16_DEPTH == 2
+    Loads L0, L1;
+    issue_loads(A, G, se, KT, NT, m, hb0, hb1, L0);
+    issue_loads(A, G, se, KT, NT, m, hb0 + 1, hb1, L1);
+    if (hb0 < hb1) {
+        dbs[0] += L0.v[2];
+        dbs[1] += L0.v[3];
+        write_planes<PL>(L0, lds, E, m);
+    }
+    __syncthreads();
+    if (active && full) hb_loop2<PL, TI, TJ, true, true>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E);
+    else if (active) hb_loop2<PL, TI, TJ, true, false>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E);
+    else if (full) hb_loop2<PL, TI, TJ, false, true>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E);
+    else hb_loop2<PL, TI, TJ, false, false>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E);
+#else
     Loads L0, L1, L2;
     issue_loads(A, G, se, KT, NT, m, hb0, hb1, L0);
     issue_loads(A, G, se, KT, NT, m, hb0 + 1, hb1, L1);
@@ -390,6 +442,7 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
     else if (active) hb_loop3<PL, TI, TJ, true, false>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
     else if (full) hb_loop3<PL, TI, TJ, false, true>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
     else hb_loop3<PL, TI, TJ, false, false>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
+#endif
 
     // partial [split][k][j], k < KT*32, j < NT*32 (32x32 C/D layout: row (r&3)+8(r>>2)+4h, col l&31)
     if (active) {

@@ -53,6 +53,13 @@ constexpr int kCompBytes = 2688 * 4;          // composite_tile's scratch (comp[
 #ifndef LNERF_K16_NOBAR
 #define LNERF_K16_NOBAR 0
 #endif
+// timing experiments only (wrong results): no encoding sincos / no compositing
+#ifndef LNERF_K16_NOPE
+#define LNERF_K16_NOPE 0
+#endif
+#ifndef LNERF_K16_NOCOMP
+#define LNERF_K16_NOCOMP 0
+#endif
 // full hidden passes get compile-time step bounds and test-free DMA issue (A/B: 0 = generic only)
 #ifndef LNERF_K16_FULLDMA
 #define LNERF_K16_FULLDMA 1
@@ -723,7 +730,12 @@ k16_fwd_bwd_kernel(K16Args a) {
                 pe[sl * kStride + c] = (float)xc;
             } else {
                 double sn, cs;
+#if LNERF_K16_NOPE   // timing experiment only (wrong results): no float64 sincos
+                sn = xc;
+                cs = xc;
+#else
                 sincos(ldexp(xc, q - 1), &sn, &cs);
+#endif
                 pe[sl * kStride + 3 + 6 * (q - 1) + c] = (float)sn;
                 pe[sl * kStride + 6 + 6 * (q - 1) + c] = (float)cs;
             }
@@ -812,7 +824,7 @@ k16_fwd_bwd_kernel(K16Args a) {
 
     // ---- rendering + loss + rendering reverse (one thread per sample, scans along rays) ----
     if (a.head_fit) comp::fit_tile(a, wg, comp, rayloss, st, a.nout);
-    else comp::composite_tile(a, wg, comp, rayloss, st);
+    else if (!LNERF_K16_NOCOMP) comp::composite_tile(a, wg, comp, rayloss, st);
     __syncthreads();
     if (tid == 0) {
         float lsum = 0.0f;

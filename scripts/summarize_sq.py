@@ -26,7 +26,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-KEEP = ("k16_fwd_bwd_kernel", "dw16_kernel", "kact_fwd_bwd_kernel", "fused_fwd_bwd_kernel",
+KEEP = ("k16_fwd_bwd_kernel", "dw16_kernel", "k32_fwd_bwd_kernel", "fused_fwd_bwd_kernel",
         "grad_reduce_kernel", "k1_reduce_kernel", "pack16_kernel", "adam_kernel")
 
 

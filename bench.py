@@ -26,7 +26,6 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "loma-nerf_amd"))
 
 METRIC = "ray-samples/sec fwd+bwd, 4096 rays×64 samples, 1/2/4/8 MI355X"
-PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA = f32 vector peak (dense)
 # bf16 MFMA dense: 256 CU x 4 SIMD x 1024 FLOP/clk (v_mfma_f32_32x32x16_bf16: 32768 FLOP / 32 clk)
 # x 2.4 GHz = 2516.6 TF; the bf16x6 split spends 6 bf16 MFMA products per fp32 multiply-add
 PEAK_BF16_TFLOPS = 2516.6
@@ -51,15 +50,11 @@ def parse():
                          "the encoding on the GPU (LNERF_INPUT_RAYS); points: host-sampled positions")
     ap.add_argument("--render", action="store_true",
                     help="config 5 instead: forward-only eval render of an 800x800 frame at 128 "
-                         "samples/ray (bf16 MFMA unless --x6/--mfma-f32), rays sharded over ranks")
+                         "samples/ray (bf16 MFMA unless --x6), rays sharded over ranks")
     ap.add_argument("--x6", action="store_true",
                     help="render with the fp32-class default split (fp16x3) instead of plain bf16")
-    ap.add_argument("--mfma-f32", action="store_true",
-                    help="fused path with exact f32 MFMA products instead of the bf16x6 split")
     ap.add_argument("--x6-train", action="store_true",
                     help="fused path with the bf16x6 split instead of the default fp16x3 split")
-    ap.add_argument("--k32", action="store_true",
-                    help="A/B: the 32-samples-per-wave k32 kernel in place of k16 (lnerf.K32)")
     ap.add_argument("--k16-w4", action="store_true",
                     help="A/B: k16 on 4-wave 64-sample workgroups, two per CU (lnerf.K16_W4)")
     ap.add_argument("--strong", action="store_true",
@@ -167,7 +162,7 @@ def bench_render(args, world, rank, local, dist, steps=None, warmup=None):
     target = torch.zeros(N, 3, dtype=torch.float32, device=dev)
     acc = torch.empty(N, 3, dtype=torch.float32, device=dev)
     loss = torch.empty(1, dtype=torch.float32, device=dev)
-    flags = lnerf.FAST | (lnerf.MFMA_F32 if args.mfma_f32 else 0 if args.x6 else lnerf.MFMA_BF16)
+    flags = lnerf.FAST | (0 if args.x6 else lnerf.MFMA_BF16)
 
     def step():
         eng.render(mlp, ws, bs, rays, None, target, samples=S, input_mode=lnerf.INPUT_RAYS,
@@ -196,8 +191,8 @@ def bench_render(args, world, rank, local, dist, steps=None, warmup=None):
     fwd_flops = 2 * sum(k * n for k, n in shapes)
     rec = None
     if rank == 0:
-        mode = "f32" if args.mfma_f32 else "fp16x3" if args.x6 else "bf16"
-        peak = PEAK_FP32_TFLOPS if args.mfma_f32 else PEAK_F16X3_TFLOPS if args.x6 else PEAK_BF16_TFLOPS
+        mode = "fp16x3" if args.x6 else "bf16"
+        peak = PEAK_F16X3_TFLOPS if args.x6 else PEAK_BF16_TFLOPS
         ach = fwd_flops * N * S / (ms / 1e3) / 1e12
         rec = {
             "metric": "ray-samples/sec fwd (eval render), 800x800 frame x 128 samples",
@@ -210,8 +205,7 @@ def bench_render(args, world, rank, local, dist, steps=None, warmup=None):
                                    "MLP 33->256x7->4, forward only",
                        "rays_per_gpu": N, "parallelism": f"replicas{world}"},
             "roofline": {"bound": "mfma",
-                         "kernel": ("fused_fwd_bwd_kernel" if args.mfma_f32 else "k16_fwd_bwd_kernel") +
-                                   " (forward only)",
+                         "kernel": "k16_fwd_bwd_kernel (forward only)",
                          "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,
                          "traffic": None,
                          "note": "rank-0 per-GPU rate: 2*sum(KN) FLOP/sample x its samples / "
@@ -279,12 +273,8 @@ def main():
     gbuf = grads[0]
     acc = torch.empty(N, 3, device=dev)
     flags = lnerf.GENERIC if args.generic else lnerf.FAST
-    if args.mfma_f32:
-        flags |= lnerf.MFMA_F32
-    elif args.x6_train:
+    if args.x6_train:
         flags |= lnerf.MFMA_BF16X6
-    if args.k32:
-        flags |= lnerf.K32
     if args.k16_w4:
         flags |= lnerf.K16_W4
 
@@ -347,7 +337,7 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
             "higher_is_better": True, "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None, "dtype": "f32",
-            "mfma": ("generic (no MFMA)" if args.generic else "f32" if args.mfma_f32 else
+            "mfma": ("generic (no MFMA)" if args.generic else
                      "bf16x6 (fp32 operands split hi+mid+lo, fp32 accumulate)" if args.x6_train else
                      "fp16x3 (fp32 operands x 2^e split hi+lo in fp16, 3 products, fp32 accumulate)"),
             "data": "synthetic (look-at camera rays, uniform targets, random-init MLP seed 215)",
@@ -366,21 +356,16 @@ def main():
         }
         if kt:
             fus_ms = kt["fused"]
-            peak = (PEAK_FP32_TFLOPS if args.mfma_f32 else PEAK_X6_TFLOPS if args.x6_train
-                    else PEAK_F16X3_TFLOPS)
-            # the fused kernel the engine ran: k16 (wave pairs, the default) or the
-            # one-wave-per-SIMD kernel (exact f32 MFMA / LNERF_ONE_WAVE)
-            lp = eng.last_path()
-            k1 = ("k16_fwd_bwd_kernel" if lp["k16"] else "k32_fwd_bwd_kernel" if lp["k32"]
-                  else "fused_fwd_bwd_kernel")
+            peak = PEAK_X6_TFLOPS if args.x6_train else PEAK_F16X3_TFLOPS
+            assert eng.last_path()["k16"], eng.last_path()
+            k1 = "k16_fwd_bwd_kernel"
             out["roofline"] = {"bound": "mfma", "kernel": k1,
                                "achieved": fused_flops / (fus_ms / 1e3) / 1e12,
                                "peak": peak, "unit": "TFLOP/s",
                                "frac": fused_flops / (fus_ms / 1e3) / 1e12 / peak,
                                "traffic": None,
                                "flops_per_launch": fused_flops, "avg_ms": fus_ms,
-                               "peak_basis": ("f32 MFMA dense 157.3 TF" if args.mfma_f32 else
-                                              "bf16 MFMA dense 2516.6 TF / 6 (bf16x6: six bf16 "
+                               "peak_basis": ("bf16 MFMA dense 2516.6 TF / 6 (bf16x6: six bf16 "
                                               "products per fp32-accurate multiply-add)" if args.x6_train
                                               else "fp16 MFMA dense 2516.6 TF / 3 (fp16x3: three fp16 "
                                               "products per multiply-add)")}
@@ -391,7 +376,7 @@ def main():
                 out["roofline"]["traffic_unit"] = "bytes/launch"
                 out["roofline"]["traffic_source"] = tr["source"]
                 out["roofline"]["traffic_gbs"] = tr["bytes"] / (fus_ms / 1e3) / 1e9
-            sq = sq_counters(k1) if full and not (args.mfma_f32 or args.x6_train) else None
+            sq = sq_counters(k1) if full and not args.x6_train else None
             if sq:
                 out["roofline"]["mfma_busy"] = sq["mfma_busy"]
                 out["roofline"]["counters"] = sq
@@ -410,7 +395,7 @@ def main():
             # config 5 (forward-only 800x800x128 bf16 eval render) on the same GPU, timed the same
             # way (its own warmup, barrier + synchronize brackets), so that it has a driver record
             eng.close()
-            r5 = bench_render(argparse.Namespace(mfma_f32=False, x6=False), 1, 0, local, None,
+            r5 = bench_render(argparse.Namespace(x6=False), 1, 0, local, None,
                               steps=5, warmup=2)
             out["config5_render"] = {k: r5[k] for k in ("metric", "value", "unit", "ms_per_step", "steps",
                                                          "warmup", "dtype", "config", "roofline")}

@@ -130,24 +130,21 @@ enum {
     LNERF_GENERIC = 8,        /* force the stage-by-stage loma-order kernels (no MFMA fusion) */
     LNERF_FAST = 16,          /* require the fused MFMA path (error if the shape is unsupported) */
     LNERF_TIMING = 32,        /* record per-kernel HIP events (read with lnerf_ctx_timings)   */
-    LNERF_MFMA_F32 = 64,      /* fused path: exact f32 MFMA products instead of the default
-                                 fp16x3 split (below)                                          */
+    LNERF_MFMA_F32 = 64,      /* removed in round 4 (the one-wave exact-f32 MFMA kernel): an
+                                 error; exact fp32 arithmetic is LNERF_GENERIC                 */
     LNERF_MFMA_BF16 = 128,    /* fused path: plain bf16 operands, fp32 accumulate (one MFMA per
                                  product; reduced precision -- inference / config 5 render)   */
-    LNERF_MFMA_F16X3 = 256,   /* fused path: the fp16x3 split, the default wherever the k16
-                                 kernel runs: x 2^e = hi + lo in fp16 with per-sample (k1) or
-                                 per-layer slab (k2) and per-layer weight exponent shifts, three
-                                 fp16 MFMAs per product, fp32 accumulate. Each product drops
+    LNERF_MFMA_F16X3 = 256,   /* fused path: the fp16x3 split, the fused path's default:
+                                 x 2^e = hi + lo in fp16 with per-sample (k1) or per-sample
+                                 balanced (k2) and per-layer weight exponent shifts, three fp16
+                                 MFMAs per product, fp32 accumulate. Each product drops
                                  <= ~3 2^-22 of its operands' shifted magnitudes, i.e. relative to
-                                 max|w| max|x| of the shift group, not to |w x| itself (values far
-                                 below their group's maximum lose bits to fp16's subnormal range).
-                                 Requesting it where k16 cannot run (a head over 16 outputs,
-                                 LNERF_ONE_WAVE) is an error.                                  */
+                                 max|w| max|x| of the shift group (one sample's row of one layer),
+                                 not to |w x| itself (values far below their row's maximum lose
+                                 bits to fp16's subnormal range).                               */
     LNERF_MFMA_BF16X6 = 512,  /* fused path: the bf16x6 split (x = hi+mid+lo in bf16, six bf16
-                                 MFMAs per product, dropped terms <= 2^-24 |w x|); the default
-                                 where k16 does not run (LNERF_ONE_WAVE, heads over 16 outputs) */
-    LNERF_K32 = 2048,         /* fused path: the k32 kernel (one wave per SIMD, 32 samples per
-                                 wave, 32x32x16 MFMAs) in place of k16                         */
+                                 MFMAs per product, dropped terms <= 2^-24 |w x|)              */
+    LNERF_K32 = 2048,         /* removed in round 4 (it lost to k16): an error                 */
     LNERF_HEAD_FIT = 8192,    /* the mlp_fit head instead of the NeRF one (scripts/mlp_fit.py:
                                  120-145, fit_img.py:423-532): sigmoid on every output channel,
                                  loss = sum over rows x outputs of (sigmoid(z) - target)^2, no
@@ -155,14 +152,16 @@ enum {
                                  image), input ENCODED (rows, k[0]), target (rows, n_out) with
                                  1 <= n_out <= 4, dists unused; acc_color receives the sigmoid
                                  outputs (rows, n_out) and d_target (rows, n_out). Runs on k16
-                                 only (LNERF_GENERIC / LNERF_ONE_WAVE / LNERF_K32 are errors). */
+                                 in fp16x3 or bf16 only (LNERF_GENERIC / LNERF_MFMA_BF16X6 are
+                                 errors).                                                      */
     LNERF_K16_W4 = 4096,      /* fused path: k16 on 4-wave, 64-sample workgroups (two per CU)
                                  instead of 8-wave, 128-sample ones (samples <= 64, fp16x3 or
-                                 plain bf16; A/B -- measured slower at cfg3)                   */
-    LNERF_ONE_WAVE = 1024     /* fused path: the one-wave-per-SIMD kernel pair
-                                 (fused_fwd_bwd_kernel + dw_all_kernel) instead of k16 + dw16,
-                                 for A/B runs; bf16x6 unless LNERF_MFMA_F32 / LNERF_MFMA_BF16.
-                                 At most one LNERF_MFMA_* precision flag may be set.            */
+                                 plain bf16, else an error; A/B -- measured slower at cfg3)     */
+    LNERF_ONE_WAVE = 1024     /* removed in round 4 (the one-wave-per-SIMD kernel pair): an error.
+                                 At most one LNERF_MFMA_* precision flag may be set; any fused-
+                                 path flag (LNERF_MFMA_*, LNERF_K16_W4) on a shape the fused path
+                                 cannot run (a head over 16 outputs, samples over 128) is an
+                                 error, as is LNERF_GENERIC together with one.                  */
 };
 
 /* Engine options (lnerf_ctx_set_option). */
@@ -214,14 +213,14 @@ int lnerf_ctx_timings(lnerf_ctx* ctx, float* ms_out, int n);
 
 /* Which kernels the last lnerf_train_step / lnerf_render on `ctx` ran (for tests and benches):
  * a mask of LNERF_PATH_* bits, the operand planes of the fused MFMAs in bits 8-9 (3 = bf16x6
- * split, 2 = fp16x3 split, 1 = plain bf16, 0 = exact f32 or the generic path), or a negative
+ * split, 2 = fp16x3 split, 1 = plain bf16, 0 = the generic path), or a negative
  * error code. 0 if no step has run. */
 enum {
     LNERF_PATH_GENERIC = 1,   /* the loma-order stage-by-stage kernels                        */
-    LNERF_PATH_FUSED = 2,     /* the fused MFMA step (any kernel pair below)                  */
+    LNERF_PATH_FUSED = 2,     /* the fused MFMA step (k16, + dw16 when training)              */
     LNERF_PATH_K16 = 4,       /* fused kernel on wave pairs (k16_fwd_bwd_kernel)              */
     LNERF_PATH_DW16 = 8,      /* dW kernel on wave pairs (dw16_kernel)                        */
-    LNERF_PATH_K32 = 16,      /* fused kernel with one wave per SIMD (k32_fwd_bwd_kernel)     */
+    LNERF_PATH_K32 = 16,      /* reserved (k32, removed in round 4)                           */
     LNERF_PATH_K16_W4 = 32    /* k16 on 4-wave, 64-sample workgroups (two per CU)             */
 };
 int lnerf_ctx_last_path(lnerf_ctx* ctx);

@@ -470,19 +470,24 @@ struct lnerf_ctx {
 };
 
 static int path_bits(const FusedPlan& p, bool train) {
-    return LNERF_PATH_FUSED | (p.k16 ? LNERF_PATH_K16 : 0) | (p.k32 ? LNERF_PATH_K32 : 0) |
-           (p.k16 && p.tile == 64 ? LNERF_PATH_K16_W4 : 0) |
-           (train && p.dw16 ? LNERF_PATH_DW16 : 0) | (p.x6 << 8);
+    return LNERF_PATH_FUSED | LNERF_PATH_K16 | (p.tile == 64 ? LNERF_PATH_K16_W4 : 0) |
+           (train ? LNERF_PATH_DW16 : 0) | (p.x6 << 8);
 }
 
-// At most one MFMA precision flag; fp16x3 only where k16 runs (it is k16's split).
+// Flags that ask for a fused-path kernel or precision: an explicit request that cannot be served
+// is an error, never a silent substitute.
+constexpr int kFusedRequests = LNERF_MFMA_BF16 | LNERF_MFMA_F16X3 | LNERF_MFMA_BF16X6 | LNERF_K16_W4;
+
+// At most one MFMA precision flag; the round-1..3 kernel selectors are gone (lnerf.h).
 static void check_precision_flags(int flags) {
-    const int prec = flags & (LNERF_MFMA_F32 | LNERF_MFMA_BF16 | LNERF_MFMA_F16X3 | LNERF_MFMA_BF16X6);
+    if (flags & (LNERF_MFMA_F32 | LNERF_ONE_WAVE | LNERF_K32))
+        fail("flags 0x%x select a removed kernel (LNERF_MFMA_F32 / LNERF_ONE_WAVE / LNERF_K32): the fused "
+             "path is k16 + dw16; exact fp32 arithmetic is LNERF_GENERIC",
+             flags & (LNERF_MFMA_F32 | LNERF_ONE_WAVE | LNERF_K32));
+    const int prec = flags & (LNERF_MFMA_BF16 | LNERF_MFMA_F16X3 | LNERF_MFMA_BF16X6);
     if (prec & (prec - 1)) fail("conflicting MFMA precision flags 0x%x (set at most one)", prec);
-}
-static void check_plan_precision(const FusedPlan& p, int flags) {
-    if ((flags & LNERF_MFMA_F16X3) && p.x6 != 2)
-        fail("LNERF_MFMA_F16X3 needs the k16 / k32 kernel (head <= 16 outputs, no LNERF_ONE_WAVE)");
+    if ((flags & LNERF_GENERIC) && (flags & kFusedRequests))
+        fail("LNERF_GENERIC conflicts with the fused-path flags 0x%x", flags & kFusedRequests);
 }
 
 extern "C" const char* lnerf_last_error(void) { return g_last_error.c_str(); }
@@ -537,8 +542,8 @@ static void validate_head(const lnerf_mlp* m, const lnerf_batch* b, int flags) {
         if (b->input_mode != LNERF_INPUT_RAYS && !b->dists) fail("null dists");
         return;
     }
-    if (flags & (LNERF_GENERIC | LNERF_ONE_WAVE | LNERF_K32 | LNERF_MFMA_F32 | LNERF_MFMA_BF16X6))
-        fail("LNERF_HEAD_FIT runs on the k16 kernel only");
+    if (flags & (LNERF_GENERIC | LNERF_MFMA_BF16X6))
+        fail("LNERF_HEAD_FIT runs on the k16 kernel in fp16x3 or bf16 only");
     if (b->samples != 1 || b->input_mode != LNERF_INPUT_ENCODED || m->n[m->num_layers - 1] > 4)
         fail("LNERF_HEAD_FIT needs samples == 1, ENCODED input and 1..4 outputs");
 }
@@ -664,6 +669,8 @@ static bool use_fused(const lnerf_mlp& m, const lnerf_batch& b, int flags) {
     const bool ok = fused_supported(m, b.rays, b.samples, b.input_mode, &why, fit);
     if (fit && !ok) fail("mlp_fit head: %s", why);
     if (!ok && (flags & LNERF_FAST)) fail("fused path unavailable: %s", why);
+    if (!ok && (flags & kFusedRequests))
+        fail("flags 0x%x ask for the fused path, which is unavailable: %s", flags & kFusedRequests, why);
     if (ok && (flags & LNERF_WANT_DX) && b.input_mode != LNERF_INPUT_ENCODED)
         fail("LNERF_WANT_DX needs ENCODED input");
     return ok;
@@ -682,21 +689,23 @@ extern "C" int lnerf_train_step(lnerf_ctx* ctx, const lnerf_mlp* mlp, const floa
         if (flags & LNERF_HEAD_FIT) o.d_dists = nullptr;
         check_precision_flags(flags);
         std::lock_guard<std::mutex> lock(ctx->mu);
+        // any failure below leaves the masks unreadable: the workspace (mask_g) may be reallocated
+        // before the step fails
+        ctx->last_k16_train = false;
         HIP_OK(hipSetDevice(ctx->device));
         hipStream_t s = (hipStream_t)stream;   // NULL: the device's default (null) stream
         if (use_fused(*mlp, *batch, flags)) {
             const size_t bytes = fused_workspace_bytes(*mlp, batch->rays, batch->samples, true, ctx->dw_grid);
             FusedPlan p{};
             fused_plan(p, *mlp, *batch, ctx->fused_ws.get(bytes), flags, true, ctx->dw_grid);
-            check_plan_precision(p, flags);
             const bool timed = (flags & LNERF_TIMING) != 0;
             fused_train_step(p, ws, bs, *batch, seed, flags, o, s, timed ? ctx->ev : nullptr);
+            check_launch("lnerf_train_step");
             ctx->timed = timed;
             ctx->last_path = path_bits(p, true);
             ctx->last_plan = p;
-            ctx->last_k16_train = p.k16 != 0 || p.k32 != 0;
+            ctx->last_k16_train = true;
         } else {
-            ctx->last_k16_train = false;
             generic_step(ctx, *mlp, ws, bs, *batch, seed, flags, o, true, s);
             ctx->timed = false;
             ctx->last_path = LNERF_PATH_GENERIC;
@@ -724,18 +733,16 @@ extern "C" int lnerf_render(lnerf_ctx* ctx, const lnerf_mlp* mlp, const float* w
         lnerf_outputs o = out ? *out : lnerf_outputs{};
         check_precision_flags(flags);
         std::lock_guard<std::mutex> lock(ctx->mu);
+        ctx->last_k16_train = false;   // a render reuses the workspace the masks live in
         HIP_OK(hipSetDevice(ctx->device));
         hipStream_t s = (hipStream_t)stream;   // NULL: the device's default (null) stream
         if (use_fused(*mlp, *batch, flags & ~LNERF_WANT_DX)) {
             const size_t bytes = fused_workspace_bytes(*mlp, batch->rays, batch->samples, false, ctx->dw_grid);
             FusedPlan p{};
             fused_plan(p, *mlp, *batch, ctx->fused_ws.get(bytes), flags, false, ctx->dw_grid);
-            check_plan_precision(p, flags);
             fused_render(p, ws, bs, *batch, o, s);
             ctx->last_path = path_bits(p, false);
-            ctx->last_k16_train = false;
         } else {
-            ctx->last_k16_train = false;
             generic_step(ctx, *mlp, ws, bs, *batch, 1.0f, 0, o, false, s);
             ctx->last_path = LNERF_PATH_GENERIC;
         }
@@ -776,8 +783,7 @@ extern "C" int lnerf_ctx_relu_masks(lnerf_ctx* ctx, unsigned char* out, size_t o
         const size_t need = (size_t)(p.L - 1) * p.R * 32;
         if (out_bytes < need) fail("relu mask buffer holds %zu bytes, needs %zu", out_bytes, need);
         HIP_OK(hipSetDevice(ctx->device));
-        if (p.k32) k32_masks_launch(p, out, (hipStream_t)stream);
-        else k16_masks_launch(p, out, (hipStream_t)stream);
+        k16_masks_launch(p, out, (hipStream_t)stream);
         check_launch("lnerf_ctx_relu_masks");
     });
 }

@@ -72,16 +72,16 @@ struct Dw16Args {
     int rpad;                   // slab positions per layer
     const int* eshift;          // per-layer product shift E_l (k1_reduce_kernel)
     int L;
-    int fmt;                    // slab tile layout: 0 = k16's, 1 = k32's (row_map)
 };
 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
 // The 16 B that thread t loads in round i (0..3) of a half-block: rounds 0, 1 are A tiles 0-3 and
 // 4-7, rounds 2, 3 G tiles 0-3 and 4-7; tile 4 (i & 1) + t / 128, and inside the tile's 512-float
-// half-block [h][n][16 f] the floats 4 (t % 128) ..+3 = features 16 h + 4 (t % 4) ..+3 of sample
-// n, with h = (t / 64) % 2 and n = (t % 64) / 4. A slab block is [tile][half-block 2][512]. The
-// per-thread part of the offset is fixed (RowMap), the half-block part is wave-uniform.
+// half-block [h][n][16 f] (k16's sample-major layout) the floats 4 (t % 128) ..+3 = features
+// 16 h + 4 (t % 4) ..+3 of sample n, with h = (t / 64) % 2 and n = (t % 64) / 4. A slab block is
+// [tile][half-block 2][512]. The per-thread part of the offset is fixed (RowMap), the half-block
+// part is wave-uniform.
 struct RowMap {
     int lane;        // per-thread float offset inside a tile's half-block
     int hstride;     // floats between the two half-blocks of a 32-sample block's tile
@@ -91,25 +91,13 @@ struct RowMap {
     bool ok[4];      // wave-uniform: the tile exists in this layer (else it is never split)
 };
 
-// fmt 0 (k16): a tile's half-block is [h 2][16 samples][16 features], thread t % 128 takes floats
-// 4 (t % 128)..+3 = features 16 h + 4 (t % 4) ..+3 of sample (t % 64) / 4, h = (t / 64) % 2.
-// fmt 1 (k32): a tile of a 32-sample block is [q 4][lane 64][4] with lane = 32 hh + sample, so
-// the half-block's part is 8 runs of 64 floats; thread u = t % 128 takes q = u / 32, hh =
-// (u / 16) % 2, sample u % 16: features 8 q + 4 hh ..+3.
-__device__ __forceinline__ RowMap row_map(int kt, int nt, int fmt) {
+__device__ __forceinline__ RowMap row_map(int kt, int nt) {
     RowMap m;
     const int t = threadIdx.x, u = t & 127;
-    if (fmt) {
-        m.lane = (u >> 5) * 256 + ((u >> 4) & 1) * 128 + (u & 15) * 4;
-        m.hstride = 64;
-        m.rowo = 8 * (u >> 5) + 4 * ((u >> 4) & 1);
-        m.isamp = u & 15;
-    } else {
-        m.lane = 4 * u;
-        m.hstride = 512;
-        m.rowo = 16 * ((t >> 6) & 1) + 4 * (t & 3);
-        m.isamp = (t & 63) >> 2;
-    }
+    m.lane = 4 * u;
+    m.hstride = 512;
+    m.rowo = 16 * ((t >> 6) & 1) + 4 * (t & 3);
+    m.isamp = (t & 63) >> 2;
     const int w2 = wave_id() >> 1;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -181,16 +169,6 @@ __device__ __forceinline__ void split4(const fx4& x, bf4& h, bf4& m, bf4& lo) {
     }
 }
 
-// The pair (x0, x1) as packed f16 hi = round(x sc), lo = round(x sc - hi) by v_fma_mix (one
-// rounding each; x sc and x sc - hi are exact): two instructions per value.
-__device__ __forceinline__ void split_h2(float x0, float x1, float sc, unsigned& hi, unsigned& lo) {
-    asm("v_fma_mixlo_f16 %0, %1, %2, 0 op_sel_hi:[0,0,0]" : "=&v"(hi) : "v"(x0), "v"(sc));
-    asm("v_fma_mixhi_f16 %0, %1, %2, 0 op_sel_hi:[0,0,0]" : "+v"(hi) : "v"(x1), "v"(sc));
-    asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel:[0,0,0] op_sel_hi:[0,0,1]"
-        : "=&v"(lo) : "v"(x0), "v"(sc), "v"(hi));
-    asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
-        : "+v"(lo) : "v"(x1), "v"(sc), "v"(hi));
-}
 
 // Split round i of the thread's values (4 features of sample n) into the plane image: 8 B per
 // plane at [plane][n][row .. row + 3]; rounds 0, 1 are A rows (shift ea), 2, 3 G rows (shift eg).
@@ -407,7 +385,7 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
 
     const float* A = a.act + a.a_off[l];
     const float* G = a.grad + a.g_off[l];
-    const RowMap m = row_map(KT, NT, a.fmt);
+    const RowMap m = row_map(KT, NT);
     // the per-sample balanced shifts (sample_shifts): every product carries 2^E, removed from the
     // partials at the end (exact)
     const unsigned short* se = a.sexp + (size_t)l * a.rpad;
@@ -568,7 +546,6 @@ void dw16_launch(const FusedPlan& p, hipStream_t s) {
     a.sexp = (const unsigned short*)p.sexp;
     a.rpad = p.num_wg * p.tile;
     a.eshift = p.dw_shift;
-    a.fmt = p.k32 ? 1 : 0;
     a.L = p.L;
     // the per-layer product shifts of k1_reduce_launch (launched right after k1)
     if (p.x6 == 2) dw16_kernel<2><<<p.dw_grid, kThreads, 0, s>>>(a);
@@ -577,10 +554,9 @@ void dw16_launch(const FusedPlan& p, hipStream_t s) {
 }
 
 void k1_reduce_launch(const FusedPlan& p, float* out_loss, hipStream_t s) {
-    const int nl = p.dw16 ? p.L : 0;
-    // k1's per-wave minima: 8 waves per workgroup for k16, 4 for k32
-    k1_reduce_kernel<<<nl + 1, 1024, 0, s>>>(p.epart, p.num_wg * (p.k32 ? 4 : p.tile / 16), p.dw_shift, nl, p.loss_part, p.num_wg,
-                                             p.loss_total, out_loss);
+    // k1's per-wave minima: tile / 16 waves per workgroup
+    k1_reduce_kernel<<<p.L + 1, 1024, 0, s>>>(p.epart, p.num_wg * (p.tile / 16), p.dw_shift, p.L, p.loss_part,
+                                              p.num_wg, p.loss_total, out_loss);
 }
 
 }  // namespace lnerf

@@ -26,6 +26,24 @@ __device__ __forceinline__ int fp16x3_shift(float m) {
     return sh > 127 ? 127 : sh;
 }
 
+// fp16x3 operand split of a pair (x0, x1), packed as two f16 per register: hi = round_f16(x sc),
+// lo = round_f16(x sc - hi), fused multiply-adds with one rounding to f16 each (x sc is exact, sc
+// a power of two; x sc - hi is exact), so |x sc - hi - lo| <= 2^-22 |x sc| in fp16's normal range.
+// Plain C on purpose: the compiler pads the MFMA wait states around these writes, which it does
+// not do inside an asm statement (a write into a register an in-flight MFMA still reads as C or
+// will write as D; tests/test_isa.py). Built with -fno-slp-vectorize (Makefile) the compiler
+// selects v_fma_mix{lo,hi}_f16 for it, 5 instructions per pair, not packed f32 math with widening
+// converts.
+__device__ __forceinline__ void split_h2(float x0, float x1, float sc, unsigned& hi, unsigned& lo) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const _Float16 h0 = (_Float16)__builtin_fmaf(x0, sc, 0.0f);
+    const _Float16 h1 = (_Float16)__builtin_fmaf(x1, sc, 0.0f);
+    const _Float16 l0 = (_Float16)__builtin_fmaf(x0, sc, -(float)h0);
+    const _Float16 l1 = (_Float16)__builtin_fmaf(x1, sc, -(float)h1);
+    hi = __builtin_bit_cast(unsigned, (h2){h0, h1});
+    lo = __builtin_bit_cast(unsigned, (h2){l0, l1});
+}
+
 // ---- ray sampling (train_nerf.py:289-306), float64 as numpy computes it -----------------------
 // t_j = np.linspace(near, far, S)[j]: j * ((far - near) / (S - 1)) + near, the last one = far.
 __host__ __device__ inline double ray_depth(int j, int S, float near_t, float far_t) {
@@ -115,27 +133,19 @@ void k_adam(float* params, const float* grads, float* m, float* v, size_t n, int
 struct FusedPlan {
     int L;
     int k[kMaxLayers], n[kMaxLayers];   // real widths
-    int kt[kMaxLayers], nt[kMaxLayers]; // 32-wide tiles
+    int kt[kMaxLayers], nt[kMaxLayers]; // 32-wide slab tiles
     int w_k, w_n;
     int rays, S, R;                     // R = rays*S
-    int tile;                           // samples per fused workgroup: 128, or 64 for k16 with
-                                        // 4-wave workgroups (two per CU; S <= 64, fp16x3 / bf16)
+    int tile;                           // samples per k16 workgroup: 128, or 64 with LNERF_K16_W4
+                                        // (4-wave workgroups, two per CU; S <= 64, fp16x3 / bf16)
     int rays_per_wg;                    // whole rays per workgroup tile
-    int num_wg;                         // fused-kernel grid
-    int blocks;                         // 32-sample slabs = num_wg * 4
+    int num_wg;                         // k1 grid
+    int blocks;                         // 32-sample slab blocks = num_wg * tile / 32
     int input_mode, F;
+    int x6;                             // operand planes: 2 = fp16x3 split (default), 3 = bf16x6
+                                        // split (both fp32-class), 1 = plain bf16 (inference)
+    int head_fit;                       // 1: the mlp_fit head (LNERF_HEAD_FIT)
     // workspace carve (device pointers)
-    float* wf;        // forward-packed weights, per layer offsets below
-    float* wb;        // backward-packed weights
-    float* bp;        // biases in fragment order
-    size_t wf_off[kMaxLayers], wb_off[kMaxLayers], bp_off[kMaxLayers];
-    int ht;           // hidden output tiles (1/2/4/8): the fused kernel's instantiation
-    int x6;           // planes per operand: 3 = bf16x6 split (fp32-accurate), 2 = fp16x3 split
-                      // (fp16 hi + lo with exponent shifts, 22-bit products; k16 only),
-                      // 1 = bf16, 0 = exact f32 MFMA
-    int fo[kMaxLayers], bo[kMaxLayers];  // packed output tiles of each layer's fwd / bwd MMA
-    unsigned short* w6;                  // bf16x6 packed planes (u16 offsets below)
-    size_t w6f_off[kMaxLayers], w6b_off[kMaxLayers], w6f_n[kMaxLayers], w6b_n[kMaxLayers];
     float* act;       // activation slabs: layer l at act_off[l], the input X slab at x_off
     size_t act_off[kMaxLayers];
     size_t x_off;
@@ -145,34 +155,24 @@ struct FusedPlan {
     float* dw_part;   // dW split partials
     float* db_part;   // dB split partials
     int dw_splits[kMaxLayers];
-    int dw_mode[kMaxLayers];       // dW kernel instantiation per layer (0 = blocked 4x4)
-    int dw_phases[kMaxLayers];     // partials per split (4 for phased small layers)
     int dw_split_off[kMaxLayers];  // workgroup offset of layer l in the dW grid
     size_t dwp_off[kMaxLayers];    // float offset of layer l's partial slabs in dw_part
     size_t dbp_off[kMaxLayers];
     int dw_grid;
     float* loss_total; // device scalar
-    // k16 kernel (lnerf_k16.hip): 512-thread workgroups, two waves per SIMD, 16x16x32 MFMA
-    int k16;                             // 1: the fused step runs k16 (pack16 + k16 kernel)
-    int head_fit;                        // 1: the mlp_fit head (LNERF_HEAD_FIT), k16 only
+    // k16 weight stream (lnerf_k16.hip): 16x16x32 MFMA, two waves per SIMD
     int ht16;                            // 16-wide hidden output tiles (1/2/4/8/16)
     int ks16_f[kMaxLayers], ks16_b[kMaxLayers];   // k-steps (32 features) per pass
     int to16_f[kMaxLayers], to16_b[kMaxLayers];   // 16-wide output tiles per pass
     unsigned short* w16;                 // packed planes, u16 offsets below
     size_t w16f_off[kMaxLayers], w16b_off[kMaxLayers];
     float* b16;                          // [L][256] zero-padded biases
-    unsigned long long* mask_g;          // [num_wg][L-1][8 waves][64 lanes] ReLU mask bits
-    int dw16;                            // 1: dW by dw16_kernel (lnerf_dw16.hip), one partial per split
-    // k32 kernel (lnerf_k32.hip): 256-thread workgroups, one wave per SIMD, 32x32x16 MFMA
-    int k32;                             // 1: the fused step runs k32 (pack32 + k32 kernel)
-    int ht32;                            // 32-wide hidden output tiles (1/2/4/8)
-    int to32_f[kMaxLayers], to32_b[kMaxLayers];     // 32-wide output tiles per pass (input tiles: ks16_*)
-    size_t w32f_off[kMaxLayers], w32b_off[kMaxLayers];   // u16 offsets into w16
+    unsigned long long* mask_g;          // [num_wg][L-1][waves][64 lanes] ReLU mask bits
     int* wexp16;                         // x6 = 2: per-layer max|W| bits (fp16 weight plane shifts)
     int* wmax_part;                      // x6 = 2: max|W| bits per layer and wmax block [L][kWmaxParts]
-    int* dw_shift;                       // dw16: per-layer product shift E_l (k1_reduce_kernel)
-    signed char* sexp;                   // dw16: k1's per-sample slab shifts [L][num_wg * 128][2]
-    int* epart;                          // dw16: k1's per-wave min of exA + exG [L][num_wg * 8]
+    int* dw_shift;                       // per-layer dW product shift E_l (k1_reduce_kernel)
+    signed char* sexp;                   // k1's per-sample slab shifts [L][num_wg * tile][2]
+    int* epart;                          // k1's per-wave min of exA + exG [L][num_wg * waves]
 };
 
 bool fused_supported(const lnerf_mlp& mlp, int rays, int S, int input_mode, const char** why,
@@ -180,7 +180,7 @@ bool fused_supported(const lnerf_mlp& mlp, int rays, int S, int input_mode, cons
 // train = false sizes the forward-only (render) workspace: packed weights + loss partials.
 // dw_grid: the dW kernel's workgroup budget (0 = kDefaultDwGrid; LNERF_OPT_DW_GRID).
 size_t fused_workspace_bytes(const lnerf_mlp& mlp, int rays, int S, bool train = true, int dw_grid = 0);
-// flags select the kernels and the MFMA precision (LNERF_MFMA_*, LNERF_ONE_WAVE; lnerf.h)
+// flags select the MFMA precision and the workgroup shape (LNERF_MFMA_*, LNERF_K16_W4; lnerf.h)
 void fused_plan(FusedPlan& p, const lnerf_mlp& mlp, const lnerf_batch& b, void* ws_base, int flags,
                 bool train = true, int dw_grid = 0);
 // ev: nullable array of 7 events recorded between the step's kernels (LNERF_TIMING)
@@ -190,21 +190,14 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
 void fused_render(const FusedPlan& p, const float* ws, const float* bs, const lnerf_batch& b,
                   const lnerf_outputs& out, hipStream_t s);
 void dw16_launch(const FusedPlan& p, hipStream_t s);
-// after a training k1: the batch loss (loss_total, out_loss) and, for dw16 with x6 = 2, the
-// layer-wide slab maxima, in one launch (lnerf_dw16.hip)
+// after a training k1: the batch loss (loss_total, out_loss) and the per-layer dW product shifts,
+// in one launch (lnerf_dw16.hip)
 void k1_reduce_launch(const FusedPlan& p, float* out_loss, hipStream_t s);
 // k16 kernel entry points (lnerf_k16.hip)
-bool k16_supported(const FusedPlan& p);
 void k16_pack(const FusedPlan& p, const float* ws, const float* bs, hipStream_t s);
 void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lnerf_outputs& out,
                 bool want_grad, hipStream_t s);
 // the last training k1's ReLU decisions as (L-1, R, 32) bytes (lnerf_ctx_relu_masks)
 void k16_masks_launch(const FusedPlan& p, unsigned char* out, hipStream_t s);
-// k32 kernel entry points (lnerf_k32.hip)
-bool k32_supported(const FusedPlan& p);
-void k32_pack(const FusedPlan& p, const float* ws, const float* bs, hipStream_t s);
-void k32_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lnerf_outputs& out,
-                bool want_grad, hipStream_t s);
-void k32_masks_launch(const FusedPlan& p, unsigned char* out, hipStream_t s);
 
 }  // namespace lnerf

@@ -133,6 +133,23 @@ struct K16Args {
 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
+// LDS byte address of a pointer into __shared__ memory.
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+    return (unsigned)(size_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// One LDS-DMA wave instruction (global_load_lds_dwordx4: 16 B per lane, lane-linear into the
+// wave-uniform LDS address `lds`), from inline asm with M0 written in the same statement.
+// Why asm: an LDS-DMA the compiler can see makes it wait vmcnt(0) before every later LDS read
+// (it cannot tell the ring slots apart), which would drain the next chunk's DMA; hidden from it,
+// the transfer has no register destination (nothing the compiler could copy or reuse early) and
+// its completion is counted by hand (dma_barrier's vmcnt). The `s_nop 0` is the M0-write ->
+// LDS-DMA wait state. No compiler code in these kernels reads M0 (tests/test_isa.py checks it).
+__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc),
+                 "s"(__builtin_amdgcn_readfirstlane(lds)));
+}
+
 // ---- optional in-kernel phase timing (-DLNERF_PROF=1, never in the product build): per-wave
 // s_memtime deltas, lane 0 accumulating in LDS, summed into g_k16_prof at the end.
 #ifndef LNERF_PROF
@@ -190,25 +207,22 @@ __device__ __forceinline__ int dma_chunk(const K16Args& a, const ChunkT& c, unsi
     int n = 0;
     if (!c.src) return 0;
     for (int off = wave * 1024; off < c.bytes; off += NW * 1024) {
-        const char* g = (const char*)c.src + off + (tid & 63) * 16;
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                         (__attribute__((address_space(3))) void*)(dst + off), 16, 0, 0);
+        glds16((const char*)c.src + off + (tid & 63) * 16, lds_addr(dst + off));
         ++n;
     }
     if (c.bias >= 0 && wave == NW - 1) {
-        const float* g = a.b16 + (size_t)c.bias * 256 + (tid & 63) * 4;
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                         (__attribute__((address_space(3))) void*)(bias_ring + (c.bias % 3) * 256),
-                                         16, 0, 0);
+        glds16(a.b16 + (size_t)c.bias * 256 + (tid & 63) * 4, lds_addr(bias_ring + (c.bias % 3) * 256));
         ++n;
     }
     return n;
 }
 
-// The chunk the next k-step reads has landed (this wave's pieces: vector-memory loads return in
-// issue order, so at most `pending` outstanding -- the pieces of the chunk after it, issued
-// later -- means every older load is done, whatever the stores in between), then s_barrier:
-// every wave's pieces are in LDS and every wave is done with the slot the next DMA overwrites.
+// The chunk the next k-step reads has landed (this wave's pieces: vector-memory operations retire
+// in issue order, so at most `pending` outstanding -- the slab stores issued after the pieces --
+// means every piece is done; compiler VM operations in between only make the wait stricter),
+// every LDS read this wave issued has returned (lgkmcnt(0): the slot the next DMA overwrites is
+// read out -- the compiler may sink the MFMAs that consume those reads below the barrier, not the
+// reads), then s_barrier: every wave's pieces are in LDS and every wave is done with that slot.
 template <int N>
 __device__ __forceinline__ void vm_wait() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -229,6 +243,7 @@ __device__ __forceinline__ void dma_barrier(int pending) {
     else if (pending == 4) vm_wait<4>();
     else if (pending > 0) vm_wait_n(pending, std::make_integer_sequence<int, 64>{});
     PROF_ADD(kPfVm, t0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #if !LNERF_K16_NOBAR   // timing experiment only (wrong results): no chunk barrier
     __builtin_amdgcn_s_barrier();
 #endif
@@ -257,18 +272,6 @@ __device__ __forceinline__ void split_h(float xs, _Float16& h, _Float16& l) {
 // of the fp16x3 scaling
 __device__ __forceinline__ int wshift_of(int maxbits) { return fp16x3_shift(__int_as_float(maxbits)); }
 
-// The same split for a pair (x0, x1) packed as two f16 per register, with v_fma_mix: hi =
-// round_f16(x sc) and lo = round_f16(x sc - hi) are fused multiply-adds with one rounding to f16
-// (x sc is exact, sc a power of two; x sc - hi is exact), two instructions per value instead of
-// scale, convert, widen, subtract and convert.
-__device__ __forceinline__ void split_h2(float x0, float x1, float sc, unsigned& hi, unsigned& lo) {
-    asm("v_fma_mixlo_f16 %0, %1, %2, 0 op_sel_hi:[0,0,0]" : "=&v"(hi) : "v"(x0), "v"(sc));
-    asm("v_fma_mixhi_f16 %0, %1, %2, 0 op_sel_hi:[0,0,0]" : "+v"(hi) : "v"(x1), "v"(sc));
-    asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel:[0,0,0] op_sel_hi:[0,0,1]"
-        : "=&v"(lo) : "v"(x0), "v"(sc), "v"(hi));
-    asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
-        : "+v"(lo) : "v"(x1), "v"(sc), "v"(hi));
-}
 
 // x = hi + mid + lo (round-to-nearest bf16 of each remainder; every remainder is exact in f32)
 __device__ __forceinline__ void split_x(float x, __bf16& h, __bf16& m, __bf16& l) {
@@ -288,25 +291,10 @@ __device__ __forceinline__ void store_slab_step(float* __restrict__ dst, const f
     __builtin_nontemporal_store(t1, (fx4*)(dst + 256 + n * 16 + 4 * g));
 }
 
-// LDS byte address of a pointer into __shared__ memory.
-__device__ __forceinline__ unsigned lds_addr(const void* p) {
-    return (unsigned)(size_t)(const __attribute__((address_space(3))) void*)p;
-}
-
-// ds_read_b128 with an immediate offset, outside the compiler's waitcnt bookkeeping: the
-// matching lgkm_wait below is the only wait, so reads of later tiles stay in flight.
+// A weight fragment: one ds_read_b128 per lane (the compiler counts it and places its wait).
 template <int OFF>
-__device__ __forceinline__ bf8 ds_read_at(unsigned addr) {
-    bf8 r;
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
-    return r;
-}
-
-// s_waitcnt lgkmcnt(N) that the fragments depend on (no use can be scheduled above it). LDS
-// reads return in order, so at most N outstanding means every older read has landed.
-template <int N>
-__device__ __forceinline__ void lgkm_wait(bf8 (&w)[3]) {
-    asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]) : "n"(N));
+__device__ __forceinline__ bf8 lds_frag(const unsigned char* base) {
+    return *(const bf8*)(base + OFF);
 }
 
 constexpr int kDist = 2;   // weight tiles read ahead of the one the MFMAs consume
@@ -319,11 +307,11 @@ constexpr int kDist = 2;   // weight tiles read ahead of the one the MFMAs consu
 #define LNERF_K16_NOSPLIT 0
 #endif
 template <int PL, int O>
-__device__ __forceinline__ void read_tile(unsigned base, bf8 (&w)[3]) {
-    w[0] = ds_read_at<(O * PL + 0) * 1024>(base);
+__device__ __forceinline__ void read_tile(const unsigned char* base, bf8 (&w)[3]) {
+    w[0] = lds_frag<(O * PL + 0) * 1024>(base);
     if constexpr (PL >= 2 && LNERF_K16_HALFLDS) w[1] = w[0];
-    else if constexpr (PL >= 2) w[1] = ds_read_at<(O * PL + 1) * 1024>(base);
-    if constexpr (PL == 3) w[2] = ds_read_at<(O * PL + 2) * 1024>(base);
+    else if constexpr (PL >= 2) w[1] = lds_frag<(O * PL + 1) * 1024>(base);
+    if constexpr (PL == 3) w[2] = lds_frag<(O * PL + 2) * 1024>(base);
 }
 
 // This wave's share of the next chunk's LDS-DMA, issued piece by piece between the MFMAs of the
@@ -345,9 +333,7 @@ struct DmaJob {
 template <int NW>
 __device__ __forceinline__ void dma_piece(const DmaJob& j, int p) {
     const int lane = threadIdx.x & 63;
-    __builtin_amdgcn_global_load_lds(
-        (const __attribute__((address_space(1))) void*)(j.src + p * (NW * 1024) + lane * 16),
-        (__attribute__((address_space(3))) void*)(j.dst + p * (NW * 1024)), 16, 0, 0);
+    glds16(j.src + p * (NW * 1024) + lane * 16, lds_addr(j.dst + p * (NW * 1024)));
 }
 // the pieces that land on output tile O: p with p * NTO / kPiecesMax == O (all on tile 0 when NTO == 1);
 // FULL: the chunk is known to be whole (every wave issues kPiecesMax pieces, no per-piece test)
@@ -356,17 +342,16 @@ __device__ __forceinline__ void dma_pieces_at(const DmaJob& j, std::integer_sequ
     (((P * NTO) / kPiecesMax == O ? ((FULL || P < j.n) ? dma_piece<NW>(j, P) : void()) : void()), ...);
 }
 
-// Output tile O of one k-step: issue the reads of tile O + kDist, wait for tile O's (leaving
-// the younger ones in flight), the MFMAs (small terms first).
+// Output tile O of one k-step: issue the reads of tile O + kDist, the MFMAs of tile O (small
+// terms first; the compiler waits for tile O's reads only, lgkmcnt(N) with the younger ones in
+// flight).
 template <int NTO, int PL, int NW, bool FD, int O>
-__device__ __forceinline__ void tile_step(unsigned base, bf8 (&w)[kDist + 1][3], const bf8& bh,
+__device__ __forceinline__ void tile_step(const unsigned char* base, bf8 (&w)[kDist + 1][3], const bf8& bh,
                                           const bf8& bm, const bf8& bl, fx4 (&out)[kMaxT], const DmaJob& job) {
     if constexpr (O + kDist < NTO) read_tile<PL, O + kDist>(base, w[(O + kDist) % (kDist + 1)]);
     if constexpr (FD) dma_pieces_at<NTO, O, NW, true>(job, std::make_integer_sequence<int, kPiecesMax>{});
     else if (job.n) dma_pieces_at<NTO, O, NW, false>(job, std::make_integer_sequence<int, kPiecesMax>{});
-    constexpr int ahead = (NTO - 1 - O) < kDist ? (NTO - 1 - O) : kDist;
     bf8(&c)[3] = w[O % (kDist + 1)];
-    lgkm_wait<ahead * (LNERF_K16_HALFLDS && PL == 2 ? 1 : PL)>(c);
     fx4 acc = out[O];
     if constexpr (PL == 2) {
         // fp16x3: small terms first (w_hi x_lo, w_lo x_hi), then w_hi x_hi; (bh, bm) = (x_hi, x_lo)
@@ -388,7 +373,7 @@ __device__ __forceinline__ void tile_step(unsigned base, bf8 (&w)[kDist + 1][3],
 
 // tiles B, B+1, ... of one k-step
 template <int NTO, int PL, int NW, bool FD, int B, int... O>
-__device__ __forceinline__ void tile_steps(std::integer_sequence<int, O...>, unsigned base,
+__device__ __forceinline__ void tile_steps(std::integer_sequence<int, O...>, const unsigned char* base,
                                            bf8 (&w)[kDist + 1][3], const bf8& bh, const bf8& bm,
                                            const bf8& bl, fx4 (&out)[kMaxT], const DmaJob& job) {
     (tile_step<NTO, PL, NW, FD, B + O>(base, w, bh, bm, bl, out, job), ...);
@@ -447,7 +432,7 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
                                          bf8& bm, bf8& bl, int& pending) {
     using R = Ring<PL, NW>;
     const int lane = threadIdx.x & 63;
-    const unsigned base = lds_addr(ring + (ci % R::slots) * R::slot_bytes) + kk * NTO * PL * 1024 + lane * 16;
+    const unsigned char* base = ring + (ci % R::slots) * R::slot_bytes + kk * NTO * PL * 1024 + lane * 16;
     const bool st = slab && !LNERF_K16_NOSTORE;
     constexpr bool spread = LNERF_K16_SPREAD && !R::stagger;
     DmaJob job;
@@ -470,10 +455,7 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
             // the biases of a first forward chunk: one more piece from the last wave, now
             issued = job.n;
             if (c.bias >= 0 && wave == NW - 1) {
-                const float* g = a.b16 + (size_t)c.bias * 256 + lane * 4;
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                                 (__attribute__((address_space(3))) void*)(bias_ring + (c.bias % 3) * 256),
-                                                 16, 0, 0);
+                glds16(a.b16 + (size_t)c.bias * 256 + lane * 4, lds_addr(bias_ring + (c.bias % 3) * 256));
                 ++issued;
             }
         } else {
@@ -631,37 +613,24 @@ __device__ __forceinline__ void store_emin(const K16Args& a, int l, int xa, int 
 }
 
 // The layer's biases in the accumulator layout (fx4 = 4 consecutive features of a lane group),
-// from its bias ring slot: ds_read_b128 outside the compiler's waitcnt bookkeeping (a plain LDS
-// read would make it wait vmcnt(0) for the in-flight weight DMA), one dependent wait per tile.
-template <int N>
-__device__ __forceinline__ void lgkm_wait4(fx4& v) {
-    asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(v) : "n"(N));
-}
-template <int OFF>
-__device__ __forceinline__ fx4 ds_read_f4(unsigned addr) {
-    fx4 r;
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
-    return r;
-}
+// from its bias ring slot (plain LDS reads: the bias DMA landed before the pass's last barrier).
 template <int NT, int... O>
-__device__ __forceinline__ void bias_read(std::integer_sequence<int, O...>, unsigned addr, fx4 (&b)[kMaxT]) {
-    ((b[O] = ds_read_f4<O * 64>(addr)), ...);
-}
-template <int NT, int... O>
-__device__ __forceinline__ void bias_wait(std::integer_sequence<int, O...>, fx4 (&b)[kMaxT]) {
-    (lgkm_wait4<NT - 1 - O>(b[O]), ...);
+__device__ __forceinline__ void bias_read(std::integer_sequence<int, O...>, const float* p, fx4 (&b)[kMaxT]) {
+    ((b[O] = *(const fx4*)(p + O * 16)), ...);
 }
 
 // ReLU and its mask bit in one short dependency chain (nerf.py:141-144): r = v > 0 ? v : 0 (NaN
 // and -0 give +0) and bits = 2 bits + (v > 0), through VCC. Written out because the compiler
 // otherwise keeps all 64 compare masks of a layer live in SGPRs and spills them to VGPR lanes.
+// In place ("+v" only): the statement writes only registers whose last writer was a compiler
+// VALU instruction (v, the sum the compiler just formed; bits, the previous statement), never an
+// MFMA operand, so no MFMA wait state can fall inside it (hipcc does not pad inside asm).
 __device__ __forceinline__ float relu_bit(float v, unsigned& bits) {
-    float r;
-    asm("v_cmp_lt_f32_e32 vcc, 0, %2\n\t"
-        "v_cndmask_b32_e32 %0, 0, %2, vcc\n\t"
+    asm("v_cmp_lt_f32_e32 vcc, 0, %0\n\t"
+        "v_cndmask_b32_e32 %0, 0, %0, vcc\n\t"
         "v_addc_co_u32_e32 %1, vcc, %1, %1, vcc"
-        : "=&v"(r), "+v"(bits) : "v"(v) : "vcc");
-    return r;
+        : "+v"(v), "+v"(bits) : : "vcc");
+    return v;
 }
 
 __device__ __forceinline__ void zero_tiles(fx4 (&t)[kMaxT]) {
@@ -779,7 +748,7 @@ k16_fwd_bwd_kernel(K16Args a) {
                                     : a.act + a.act_off[l - 1] + blk * (size_t)(a.kt[l] * 1024)) +
                                 half * 512;
         zero_tiles(out);
-        const unsigned bl = lds_addr(bias_ring + (l % 3) * 256) + g * 16;
+        const float* bl = bias_ring + (l % 3) * 256 + g * 4;
         const float xm = (PL >= 2 || st) ? sample_max(act) : 0.0f;
         if (st) exa.put(l, store_sexp(a, l, 0, xm));
         const int ex = shift_of(xm);
@@ -792,7 +761,6 @@ k16_fwd_bwd_kernel(K16Args a) {
             // bias after the sum (nerf.py:98,125), ReLU (nerf.py:141-144) and its mask bits
             fx4 bv[kMaxT];
             bias_read<HT>(std::make_integer_sequence<int, HT>{}, bl, bv);
-            bias_wait<HT>(std::make_integer_sequence<int, HT>{}, bv);
             // values in descending bit order (feature 4o + i ends in bit 4o + i of lo / hi)
             unsigned mlo = 0u, mhi = 0u;
 #pragma unroll
@@ -810,7 +778,6 @@ k16_fwd_bwd_kernel(K16Args a) {
             k16_pass<1, PL, NW>(a, a.ks_f[l], ci, ring, bias_ring, act, out, slab, ex);
             fx4 bv[kMaxT];
             bias_read<1>(std::make_integer_sequence<int, 1>{}, bl, bv);
-            bias_wait<1>(std::make_integer_sequence<int, 1>{}, bv);
             // head pre-activations: features 0..3 = registers 0..3 of lane group 0
             if (g == 0) {
 #pragma unroll
@@ -1016,12 +983,6 @@ void k16_masks_launch(const FusedPlan& p, unsigned char* out, hipStream_t s) {
     if (n == 0) return;
     k16_masks_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(p.mask_g, p.L - 1, p.R, p.rays_per_wg * p.S,
                                                                  p.tile / 16, out);
-}
-
-bool k16_supported(const FusedPlan& p) {
-    if (p.x6 != 3 && p.x6 != 2 && p.x6 != 1) return false;
-    if (p.n[p.L - 1] > 16) return false;       // head: one 16-wide output tile
-    return true;
 }
 
 void k16_pack(const FusedPlan& p, const float* ws, const float* bs, hipStream_t s) {

@@ -28,12 +28,12 @@ WANT_DX = 4
 GENERIC = 8
 FAST = 16
 TIMING = 32
-MFMA_F32 = 64     # fused path: exact f32 MFMA instead of the default fp16x3 split
+MFMA_F32 = 64     # removed in round 4 (one-wave exact-f32 kernel): an error; exact fp32 is GENERIC
 MFMA_BF16 = 128   # fused path: plain bf16 operands (reduced precision; inference)
 MFMA_F16X3 = 256  # fused path: fp16x3 split (22-bit products, fp32 accumulate; the k16 default)
 MFMA_BF16X6 = 512  # fused path: bf16x6 split (fp32-accurate products)
-ONE_WAVE = 1024    # fused path: the one-wave-per-SIMD kernel pair instead of k16 + dw16 (A/B)
-K32 = 2048         # fused path: the 32-samples-per-wave 32x32 MFMA kernel instead of k16 (A/B)
+ONE_WAVE = 1024    # removed in round 4 (the one-wave-per-SIMD kernel pair): an error
+K32 = 2048         # removed in round 4 (k32 lost to k16): an error
 K16_W4 = 4096      # fused path: k16 on 4-wave 64-sample workgroups, two per CU (A/B)
 HEAD_FIT = 8192    # the mlp_fit head (sigmoid on every output, no compositing; samples = 1)
 
@@ -53,7 +53,7 @@ PATH_GENERIC = 1
 PATH_FUSED = 2
 PATH_K16 = 4
 PATH_DW16 = 8
-PATH_K32 = 16
+PATH_K32 = 16      # reserved (k32, removed in round 4)
 PATH_K16_W4 = 32
 
 
@@ -294,7 +294,7 @@ class Engine:
                input_mode: int = INPUT_POINTS, num_freqs: int = 5, near: float = 2.0,
                far: float = 6.0, flags: int = 0, acc=None, loss=None):
         """Forward only (train_nerf.py:616-661 eval render): (loss, acc_color). flags may select
-        MFMA_BF16 (the config-5 inference precision), MFMA_F32 or GENERIC."""
+        MFMA_BF16 (the config-5 inference precision), MFMA_BF16X6 or GENERIC."""
         torch = self.torch
         rays = target.shape[0]
         b = self._batch(rays, samples, input_mode, num_freqs, x, dists, target, near, far)
@@ -338,8 +338,7 @@ class Engine:
         if v < 0:
             raise RuntimeError(f"lnerf_ctx_last_path: {last_error()}")
         return dict(generic=bool(v & PATH_GENERIC), fused=bool(v & PATH_FUSED),
-                    k16=bool(v & PATH_K16), dw16=bool(v & PATH_DW16), k32=bool(v & PATH_K32),
-                    k16_w4=bool(v & PATH_K16_W4),
+                    k16=bool(v & PATH_K16), dw16=bool(v & PATH_DW16), k16_w4=bool(v & PATH_K16_W4),
                     planes=(v >> 8) & 3)
 
     def relu_masks(self, L: int, R: int):

@@ -1,7 +1,7 @@
 # One GPU session = a list of named steps, each under its own time limit, stopping at the first
 # failure (a fault, abort, time limit or failing test ends the call):
 #   gpurun -- bash scripts/gpu_steps.sh tests bench trace sq
-# steps: tests | bench | k32 | k32trace | dist | render | precision | trace | pmc | sq | compat
+# steps: tests | bench | dist | render | precision | trace | pmc | sq | compat
 # Logs go to gpurun_out/<step>.log; rocprof output under gpurun_out/prof and gpurun_out/sq.
 set -u
 cd "$GRAFT_REPO_ROOT"
@@ -17,17 +17,6 @@ for step in "$@"; do
     bench)
       timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1
       rc=$?; tail -1 gpurun_out/bench.log | cut -c1-900 ;;
-    k32)
-      timeout -k 10 300 python -u -m pytest tests/test_gpu_native.py -m gpu -x -q -p no:cacheprovider \
-        --timeout 120 --timeout-method thread -k "2048 or 2560" > gpurun_out/k32tests.log 2>&1 &&
-      timeout -k 10 300 python bench.py --k32 --no-cpu-baseline --no-render > gpurun_out/k32bench.log 2>&1
-      rc=$?; tail -3 gpurun_out/k32tests.log; tail -1 gpurun_out/k32bench.log | cut -c1-900 ;;
-    k32trace)
-      mkdir -p gpurun_out/prof
-      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
-        -d "$R/gpurun_out/prof/k32trace" -o run -- python3 "$R/bench.py" --k32 --steps 10 --warmup 3 \
-        --no-cpu-baseline > "$R/gpurun_out/prof/k32trace.log" 2>&1)
-      rc=$? ;;
     dist)
       timeout -k 10 300 python -u -m pytest tests/test_gpu_dist.py -m gpu -x -v -p no:cacheprovider \
         --timeout 120 --timeout-method thread > gpurun_out/dist.log 2>&1 &&

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Accuracy of each step implementation against the float64 numpy restatement (oracle/nerf_np.py)
 on a cfg3 subset (the bench MLP 33->256x7->4, 64 samples): the C loma-order fp32 oracle, the
-generic device path, the fused path with exact f32 MFMA, with the fp16x3 split (k16 + dw16, the
-default), with the bf16x6 split (k16 + dw16) and the one-wave-per-SIMD bf16x6 kernel (LNERF_ONE_WAVE). Reported twice: on all rays, and
+generic device path, the fused path with the fp16x3 split (k16 + dw16, the default) and with the
+bf16x6 split (k16 + dw16). Reported twice: on all rays, and
 without the rays holding a ReLU decision below fp32 resolution (nerf_np.relu_tie_rays: |z| <
 5e-7 sum|terms|, where any fp32 summation order may decide either way and the flipped sample's
 whole gradient row moves). Test/report infrastructure (imports the oracle); writes
@@ -59,10 +59,8 @@ def report(eng, w):
     ref = f64_reference(w)
     rep = {"oracle_c_fp32": errors(oracle_ref(w, seed=1.0), ref),
            "generic_device": errors(run_native(eng, w, seed=1.0, flags=lnerf.GENERIC), ref),
-           "fused_f32_mfma": errors(run_native(eng, w, seed=1.0, flags=lnerf.FAST | lnerf.MFMA_F32), ref),
            "fused_f16x3_k16_dw16": errors(run_native(eng, w, seed=1.0, flags=lnerf.FAST), ref),
            "fused_bf16x6_k16_dw16": errors(run_native(eng, w, seed=1.0, flags=lnerf.FAST | lnerf.MFMA_BF16X6), ref)}
-    rep["fused_bf16x6_one_wave_kernels"] = errors(run_native(eng, w, seed=1.0, flags=lnerf.FAST | lnerf.ONE_WAVE), ref)
     return rep
 
 

@@ -74,7 +74,7 @@ def run_fused(engine, w, *, points=True, seed=None, flags=0, want_dx=False):
         out["dX"] = r.d_x.cpu().numpy()
     L = len(shapes)
     path = engine.last_path()
-    assert path["k32"] if flags & lnerf.K32 else path["k16"], path
+    assert path["k16"], path
     m = engine.relu_masks(L, w.N * w.S)
     out["masks"] = [m[l, :, :shapes[l][1]] for l in range(L - 1)]
     return out

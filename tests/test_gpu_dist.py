@@ -67,7 +67,7 @@ def test_rccl_step_equals_single_gpu_loss_seeded(engine, nccl, rays):
         dp.allreduce_loss_seeded(gb[0], nccl, engine.scale_by_device_scalar)
         engine.adam_update(pb, gb[0][:-1], mb, vb, it, 5e-4)
         torch.cuda.synchronize()
-        assert engine.last_path()["k16"] or engine.last_path()["k32"]
+        assert engine.last_path()["k16"]
         assert torch.isfinite(ga[0]).all()
         assert float(ga[0][-1]) == float(gb[0][-1]), it           # the loss slot
         assert torch.equal(ga[0], gb[0]), (it, (ga[0] - gb[0]).abs().max().item())

@@ -19,7 +19,12 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-PRECS = {"fp16x3": 0, "bf16x6": 512, "f32_one_wave": 64, "generic": 8}
+PRECS = {"fp16x3": 0, "bf16x6": 512, "generic": 8}
+# fp16x3 dW, per column: |err| <= 1e-4 x the column's own max (the bar of
+# test_gpu_native.py::test_full_size_all_rays_float64); the layer-relative bound below is the
+# documented one (include/lnerf.h, LNERF_MFMA_F16X3), the per-column one is what k2's per-sample
+# balanced shifts deliver on these fixtures (lnerf_dw16.hip sample_shifts)
+F16X3_COL_TOL = 1e-4
 
 
 def load(name):
@@ -76,17 +81,20 @@ def test_edge_numerics(engine, name, prec):
     close_grouped("d_target", got["d_target"], g["d_target"])
     close_grouped("d_dists", got["d_dists"], g["d_dists"])
     if prec == "fp16x3":
-        # dw16's fp16x3 split shifts each slab by its layer-wide maximum, so a dW column far below
-        # its layer's largest (here the sigma column, dsigma ~ 1e8) keeps ~11-22 bits: its error
-        # bound is layer-relative (include/lnerf.h, LNERF_MFMA_F16X3). Checked against that bound,
-        # and the per-column figure is reported.
+        # the fp16x3 products keep 22 bits relative to their shift group (one sample's A row and
+        # G row, balanced per sample by k2), so the bound is checked twice: layer-relative as
+        # documented, and per column against F16X3_COL_TOL -- the sigma column (dsigma ~ 1e8 on the
+        # delta = 1e8 rays) dominates its layer's max, so the layer bound alone would leave the
+        # other columns unchecked.
         close_grouped("dW", got["dW"].reshape(g["dW"].shape[0], -1), g["dW"].reshape(g["dW"].shape[0], -1),
                       gtol=2e-6)
         w = np.where(np.isnan(g["dW"]), 0, g["dW"])
         e = np.abs(np.where(np.isnan(g["dW"]), 0, got["dW"] - w)).max(axis=1)
         cm = np.abs(w).max(axis=1)
-        print(f"{name} fp16x3 worst per-column dW error / column max: "
-              f"{(e[cm > 0] / cm[cm > 0]).max():.3g}")
+        worst = float((e[cm > 0] / cm[cm > 0]).max())
+        print(f"{name} fp16x3 worst per-column dW error / column max: {worst:.3g}")
+        assert worst <= F16X3_COL_TOL, worst
+        close_grouped("dW", got["dW"], g["dW"], rtol=1e-5, gtol=F16X3_COL_TOL)
     else:
         close_grouped("dW", got["dW"], g["dW"])
     close_grouped("dB", got["dB"], g["dB"])

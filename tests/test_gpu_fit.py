@@ -161,6 +161,6 @@ def test_mlp_fit_head_rejects_unsupported_calls(engine, fit):
     dev = "cuda:0"
     mlp = lnerf.make_mlp(shapes, wp.shape[1], wp.shape[2])
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a[:64])).to(dev)
-    for bad in (lnerf.GENERIC, lnerf.ONE_WAVE, lnerf.K32, lnerf.MFMA_F32):
+    for bad in (lnerf.GENERIC, lnerf.ONE_WAVE, lnerf.K32, lnerf.MFMA_F32, lnerf.MFMA_BF16X6):
         with pytest.raises(RuntimeError):
             engine.mlp_fit_step(mlp, t(wp), t(bp), t(X), t(T), seed=1.0, flags=bad)

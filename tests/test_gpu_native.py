@@ -2,12 +2,11 @@
 the C oracle, plus size-independent properties at the full bench size (4096 rays x 64 samples,
 8x256 MLP).
 
-The default path (k16 + dw16, fp16x3 split) and its bf16x6 variant are checked on EVERY ray with
-tests/fused_parity.py: float64 at the GPU's own ReLU decisions within 1e-5 (abs + max-scaled),
-every decision that differs from float64's a tie at fp32 resolution, and the loma-order fp32
-oracle on the rays whose decisions agree with its own. The one-wave kernel pair (exact f32 MFMA,
-LNERF_ONE_WAVE) keeps its masks in LDS, so its tests compare with the C oracle on the rays that
-hold no decision below fp32 resolution (nerf_np.without_relu_ties).
+The default path (k16 + dw16, fp16x3 split) and its bf16x6 / 4-wave variants are checked on EVERY
+ray with tests/fused_parity.py: float64 at the GPU's own ReLU decisions within 1e-5 (abs +
+max-scaled), every decision that differs from float64's a tie at fp32 resolution, and the
+loma-order fp32 oracle on the rays whose decisions agree with its own. The kernel selectors of
+rounds 1-3 (LNERF_MFMA_F32 / LNERF_ONE_WAVE / LNERF_K32) are errors since round 4.
 
 Tolerance forms: |got - want| <= rtol |want| + atol_scale max|want| per tensor (loma_calls.py).
 """
@@ -20,8 +19,7 @@ from loma_calls import assert_close
 
 pytestmark = pytest.mark.gpu
 
-TOL = dict(rtol=1e-4, atol_scale=1e-4)       # north_star's 1e-4 (one-wave paths, vs C oracle)
-TOL_F32 = dict(rtol=1e-5, atol_scale=1e-5)   # exact f32 MFMA vs the C oracle
+TOL = dict(rtol=1e-4, atol_scale=1e-4)       # north_star's 1e-4 (vs the C oracle)
 
 
 def _dev(engine, a):
@@ -68,35 +66,19 @@ def compare(got, want, keys=("dW", "dB", "d_dists", "d_target"), tol=TOL):
 
 FUSED = [0, 512, 4096]   # k16 + dw16: default fp16x3 split, lnerf.MFMA_BF16X6, lnerf.K16_W4 (fp16x3
                           # on 4-wave 64-sample workgroups, two per CU, instead of one 8-wave one)
-K32 = [2048, 2048 | 512]  # lnerf.K32 (32 samples per wave, 32x32 MFMA) + dw16: fp16x3, bf16x6
-ONE_WAVE = [64, 1024]  # one-wave pair: lnerf.MFMA_F32 (exact f32), lnerf.ONE_WAVE (bf16x6)
 
 
-def _one_wave_tol(prec):
-    return TOL_F32 if prec == 64 else TOL
-
-
-@pytest.mark.parametrize("prec", FUSED + K32)
+@pytest.mark.parametrize("prec", FUSED)
 @pytest.mark.parametrize("points", [True, False])
 def test_fused_cfg2_all_rays(engine, points, prec):
     """Config 2 (train_nerf-sized MLP 33->30->30->4), 1024 rays x 32 samples, seed = loss."""
     check_fused(engine, nerf_np.make_workload("cfg2"), points=points, flags=prec)
 
 
-@pytest.mark.parametrize("prec", FUSED + K32)
+@pytest.mark.parametrize("prec", FUSED)
 def test_fused_cfg3_subset_all_rays(engine, prec):
     """The bench MLP (33->256x7->4) on 48 rays x 64 samples, seed = loss."""
     check_fused(engine, nerf_np.make_workload("cfg3", rays=48), flags=prec)
-
-
-@pytest.mark.parametrize("prec", ONE_WAVE)
-@pytest.mark.parametrize("cfg", ["cfg2", "cfg3"])
-def test_one_wave_matches_oracle(engine, cfg, prec):
-    w = nerf_np.without_relu_ties(nerf_np.make_workload(cfg, rays=24 if cfg == "cfg3" else None))
-    got = run_native(engine, w, flags=prec)
-    path = engine.last_path()
-    assert path["fused"] and not path["k16"] and not path["dw16"], path
-    compare(got, oracle_ref(w), tol=_one_wave_tol(prec))
 
 
 def _nonuniform(w):
@@ -112,7 +94,7 @@ def _nonuniform(w):
     return nerf_np.Workload(w.pts, w.pts32, w.X, w.dists, w.target, ws, bs, wp2, bp2, w.F, w.S, w.N)
 
 
-@pytest.mark.parametrize("prec", FUSED + K32)
+@pytest.mark.parametrize("prec", FUSED)
 def test_fused_nonuniform_widths(engine, prec):
     """Hidden widths that differ per layer (33->128->256->64->100->4): every layer's MMA runs
     with the widest layer's tile count over zero-padded packed weights."""
@@ -128,60 +110,84 @@ def _deep(w):
     return nerf_np.Workload(w.pts, w.pts32, w.X, w.dists, w.target, ws, bs, wp, bp, w.F, w.S, w.N)
 
 
-@pytest.mark.parametrize("prec", FUSED + K32 + ONE_WAVE + [128])
+@pytest.mark.parametrize("prec", FUSED + [128])
 def test_fused_deep_mlp(engine, prec):
     """12 layers (33->64x11->4): the k16 kernel's chunk stream (2 passes x 11 hidden layers) and
-    its HBM ReLU masks beyond the 8 hidden layers the one-wave kernel keeps in LDS. The bf16
-    precisions run on k16 (+ dw16 for the splits); MFMA_F32 on the one-wave kernel, which falls
-    back to exact f32 past its mask budget (LNERF_ONE_WAVE too)."""
+    its HBM ReLU masks. The split precisions against float64 on every ray; plain bf16 (128, the
+    render precision) against the oracle with a loose bound."""
     import lnerf
     w = _deep(nerf_np.make_workload("cfg2", rays=32, samples=32))
-    if prec in FUSED + K32:
+    if prec in FUSED:
         check_fused(engine, w, flags=prec)
-        k32 = bool(prec & lnerf.K32)
-        w4 = bool(prec & lnerf.K16_W4)
-        assert engine.last_path() == dict(generic=False, fused=True, k16=not k32, dw16=True, k32=k32,
-                                          k16_w4=w4, planes=3 if prec & lnerf.MFMA_BF16X6 else 2)
+        assert engine.last_path() == dict(generic=False, fused=True, k16=True, dw16=True,
+                                          k16_w4=bool(prec & lnerf.K16_W4),
+                                          planes=3 if prec & lnerf.MFMA_BF16X6 else 2)
         return
-    got = run_native(engine, nerf_np.without_relu_ties(w) if prec != 128 else w,
-                     flags=lnerf.FAST | prec)
-    path = engine.last_path()
-    if prec == 128:
-        # plain bf16 operands (8 significant bits): a loose sanity bound, not the fp32 tolerance
-        assert path == dict(generic=False, fused=True, k16=True, dw16=True, k32=False, k16_w4=False,
-                            planes=1), path
-        want = oracle_ref(w)
-        assert abs(got["loss"] - want["loss"]) <= 2e-2 * abs(want["loss"]), (got["loss"], want["loss"])
-        assert_close("dW", got["dW"], want["dW"], rtol=0.0, atol_scale=5e-2)
-    else:
-        assert path == dict(generic=False, fused=True, k16=False, dw16=False, k32=False, k16_w4=False,
-                            planes=0), path
-        compare(got, oracle_ref(nerf_np.without_relu_ties(w)), tol=TOL_F32)
+    got = run_native(engine, w, flags=lnerf.FAST | prec)
+    # plain bf16 operands (8 significant bits): a loose sanity bound, not the fp32 tolerance
+    assert engine.last_path() == dict(generic=False, fused=True, k16=True, dw16=True, k16_w4=False,
+                                      planes=1)
+    want = oracle_ref(w)
+    assert abs(got["loss"] - want["loss"]) <= 2e-2 * abs(want["loss"]), (got["loss"], want["loss"])
+    assert_close("dW", got["dW"], want["dW"], rtol=0.0, atol_scale=5e-2)
 
 
 def test_default_path_is_k16_dw16(engine):
-    """The bench configuration (cfg3 MLP) runs k16 + dw16 with the fp16x3 split by default, the
-    one-wave pair with bf16x6 under LNERF_ONE_WAVE; conflicting precision flags and an fp16x3
-    request the k16 kernel cannot serve are errors."""
+    """The bench configuration (cfg3 MLP) runs k16 + dw16 with the fp16x3 split by default.
+    Errors, never silent substitutes: conflicting precision flags, the removed kernel selectors
+    (MFMA_F32 / ONE_WAVE / K32), K16_W4 where it cannot run (bf16x6, samples > 64), a fused-path
+    flag on a shape the fused path does not take (a 20-output head), GENERIC with a fused flag."""
     import lnerf
     w = nerf_np.make_workload("cfg3", rays=8)
     run_native(engine, w, per_ray=False)
-    assert engine.last_path() == dict(generic=False, fused=True, k16=True, dw16=True, k32=False, k16_w4=False,
-                                      planes=2)
+    assert engine.last_path() == dict(generic=False, fused=True, k16=True, dw16=True, k16_w4=False, planes=2)
     run_native(engine, w, per_ray=False, flags=lnerf.K16_W4)
     assert engine.last_path()["k16"] and engine.last_path()["k16_w4"]
     run_native(engine, w, per_ray=False, flags=lnerf.MFMA_F16X3)
     assert engine.last_path()["planes"] == 2
-    run_native(engine, w, per_ray=False, flags=lnerf.ONE_WAVE)
-    assert engine.last_path() == dict(generic=False, fused=True, k16=False, dw16=False, k32=False,
-                                      k16_w4=False, planes=3)
-    for bad in (lnerf.ONE_WAVE | lnerf.MFMA_F16X3, lnerf.MFMA_F16X3 | lnerf.MFMA_BF16X6,
-                lnerf.MFMA_BF16 | lnerf.MFMA_BF16X6):
+    for bad in (lnerf.MFMA_F16X3 | lnerf.MFMA_BF16X6, lnerf.MFMA_BF16 | lnerf.MFMA_BF16X6,
+                lnerf.MFMA_F32, lnerf.ONE_WAVE, lnerf.K32, lnerf.K16_W4 | lnerf.MFMA_BF16X6,
+                lnerf.GENERIC | lnerf.MFMA_BF16):
         with pytest.raises(RuntimeError):
             run_native(engine, w, per_ray=False, flags=bad)
+    with pytest.raises(RuntimeError):   # K16_W4 needs whole rays in 64 samples
+        run_native(engine, nerf_np.make_workload("cfg2", rays=4, samples=100), per_ray=False,
+                   flags=lnerf.K16_W4)
     # the relu mask readout exists only after a k16 training step
     with pytest.raises(RuntimeError):
         engine.relu_masks(8, 8 * 64)
+
+
+def test_failed_step_invalidates_relu_masks(engine):
+    """a k16 step, then a failing call on a larger batch (the workspace may have been
+    reallocated before the failure): the mask readout must raise, not read freed memory."""
+    import lnerf
+    small = nerf_np.make_workload("cfg2", rays=16)
+    run_native(engine, small, per_ray=False)
+    engine.relu_masks(3, 16 * 32)   # valid right after the k16 step
+    big = nerf_np.make_workload("cfg2", rays=2048)
+    with pytest.raises(RuntimeError):   # fails in the flag check, after the lock
+        run_native(engine, big, per_ray=False, flags=lnerf.K16_W4 | lnerf.MFMA_BF16X6)
+    with pytest.raises(RuntimeError):
+        engine.relu_masks(3, 16 * 32)
+
+
+def test_wide_head_runs_generic_or_fails(engine):
+    """A head over 16 outputs is outside the fused path: the default call runs the loma-order
+    kernels, a fused-path request is an error."""
+    import lnerf
+    w = nerf_np.make_workload("cfg2", rays=8, samples=16)
+    rng = np.random.RandomState(11)
+    ws = list(w.ws[:-1]) + [(rng.randn(w.ws[-1].shape[0], 20) * 0.1).astype(np.float32)]
+    bs = list(w.bs[:-1]) + [(rng.randn(20) * 0.1).astype(np.float32)]
+    wp, bp = nerf_np.pad_weights(ws, bs)
+    wide = nerf_np.Workload(w.pts, w.pts32, w.X, w.dists, w.target, ws, bs, wp, bp, w.F, w.S, w.N)
+    run_native(engine, wide, per_ray=False)
+    assert engine.last_path()["generic"]
+    with pytest.raises(RuntimeError):
+        run_native(engine, wide, per_ray=False, flags=lnerf.FAST)
+    with pytest.raises(RuntimeError):
+        run_native(engine, wide, per_ray=False, flags=lnerf.MFMA_BF16X6)
 
 
 def test_dw_grid_option(engine):
@@ -329,7 +335,7 @@ def test_full_size_oracle_rays_spotcheck(engine, full):
 
 # ---- against the committed golden fixtures (float64 numpy restatement) ------------------------
 
-@pytest.mark.parametrize("prec", FUSED + K32 + ONE_WAVE)
+@pytest.mark.parametrize("prec", FUSED)
 @pytest.mark.parametrize("name", ["chunk_4x30.npz", "deep8_w64_2x64.npz", "trained_weights_8x16.npz"])
 def test_fused_matches_golden_fixture(engine, name, prec):
     import os
@@ -345,7 +351,7 @@ def test_fused_matches_golden_fixture(engine, name, prec):
                           samples=S, input_mode=lnerf.INPUT_ENCODED, seed=1.0, want_per_ray=True,
                           want_dx=True, flags=lnerf.FAST | prec)
     torch.cuda.synchronize()
-    tol = TOL64 if prec in FUSED + K32 else _one_wave_tol(prec)
+    tol = TOL64
     assert abs(float(r.loss.item()) - g["loss"]) <= 1e-6 * abs(g["loss"])
     assert_close("acc", r.acc_color.cpu().numpy(), g["acc"], **tol)
     assert_close("dW", r.d_ws.cpu().numpy(), g["dW"], **tol)

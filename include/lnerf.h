@@ -157,6 +157,9 @@ enum {
     LNERF_K16_W4 = 4096,      /* fused path: k16 on 4-wave, 64-sample workgroups (two per CU)
                                  instead of 8-wave, 128-sample ones (samples <= 64, fp16x3 or
                                  plain bf16, else an error; A/B -- measured slower at cfg3)     */
+    LNERF_RENDER_K16 = 16384, /* lnerf_render in plain bf16: k16's forward (one 16-sample group
+                                 per wave) instead of kr (lnerf_render.hip: two groups per wave,
+                                 each weight fragment read from LDS feeds both; A/B)           */
     LNERF_ONE_WAVE = 1024     /* removed in round 4 (the one-wave-per-SIMD kernel pair): an error.
                                  At most one LNERF_MFMA_* precision flag may be set; any fused-
                                  path flag (LNERF_MFMA_*, LNERF_K16_W4) on a shape the fused path
@@ -205,9 +208,10 @@ int lnerf_get_rays(int width, const double* K, const double* c2w, float* rays, v
 int lnerf_render(lnerf_ctx* ctx, const lnerf_mlp* mlp, const float* ws, const float* bs,
                  const lnerf_batch* batch, int flags, const lnerf_outputs* out, void* stream);
 
-/* Per-kernel times (ms) of the last LNERF_TIMING step on `ctx`, measured with HIP events on the
- * step's stream: [0] weight pack, [1] fused fwd+reverse-chain kernel, [2] loss reduce,
- * [3] dW kernel, [4] dW/db reduce, [5] whole step. Synchronises on the step. Returns the number
+/* Per-kernel times (ms) of the last LNERF_TIMING step or render on `ctx`, measured with HIP events
+ * on its stream: [0] weight pack, [1] fused fwd+reverse-chain kernel (a render: the forward
+ * kernel), [2] loss reduce, [3] dW kernel, [4] dW/db reduce, [5] whole step (0 for the kernels a
+ * render does not run). Synchronises on the step. Returns the number
  * of values written (0 if no timed step ran on the fused path). */
 int lnerf_ctx_timings(lnerf_ctx* ctx, float* ms_out, int n);
 
@@ -221,7 +225,8 @@ enum {
     LNERF_PATH_K16 = 4,       /* fused kernel on wave pairs (k16_fwd_bwd_kernel)              */
     LNERF_PATH_DW16 = 8,      /* dW kernel on wave pairs (dw16_kernel)                        */
     LNERF_PATH_K32 = 16,      /* reserved (k32, removed in round 4)                           */
-    LNERF_PATH_K16_W4 = 32    /* k16 on 4-wave, 64-sample workgroups (two per CU)             */
+    LNERF_PATH_K16_W4 = 32,   /* k16 on 4-wave, 64-sample workgroups (two per CU)             */
+    LNERF_PATH_KR = 64        /* the render ran kr (lnerf_render.hip), not k16's forward      */
 };
 int lnerf_ctx_last_path(lnerf_ctx* ctx);
 

@@ -476,7 +476,8 @@ static int path_bits(const FusedPlan& p, bool train) {
 
 // Flags that ask for a fused-path kernel or precision: an explicit request that cannot be served
 // is an error, never a silent substitute.
-constexpr int kFusedRequests = LNERF_MFMA_BF16 | LNERF_MFMA_F16X3 | LNERF_MFMA_BF16X6 | LNERF_K16_W4;
+constexpr int kFusedRequests = LNERF_MFMA_BF16 | LNERF_MFMA_F16X3 | LNERF_MFMA_BF16X6 | LNERF_K16_W4 |
+                               LNERF_RENDER_K16;
 
 // At most one MFMA precision flag; the round-1..3 kernel selectors are gone (lnerf.h).
 static void check_precision_flags(int flags) {
@@ -740,9 +741,12 @@ extern "C" int lnerf_render(lnerf_ctx* ctx, const lnerf_mlp* mlp, const float* w
             const size_t bytes = fused_workspace_bytes(*mlp, batch->rays, batch->samples, false, ctx->dw_grid);
             FusedPlan p{};
             fused_plan(p, *mlp, *batch, ctx->fused_ws.get(bytes), flags, false, ctx->dw_grid);
-            fused_render(p, ws, bs, *batch, o, s);
-            ctx->last_path = path_bits(p, false);
+            const bool timed = (flags & LNERF_TIMING) != 0;
+            fused_render(p, ws, bs, *batch, o, s, flags, timed ? ctx->ev : nullptr);
+            ctx->timed = timed;
+            ctx->last_path = path_bits(p, false) | (fused_render_uses_kr(p, flags) ? LNERF_PATH_KR : 0);
         } else {
+            ctx->timed = false;
             generic_step(ctx, *mlp, ws, bs, *batch, 1.0f, 0, o, false, s);
             ctx->last_path = LNERF_PATH_GENERIC;
         }

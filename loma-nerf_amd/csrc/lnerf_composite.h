@@ -1,8 +1,9 @@
 // lnerf_composite.h -- per-sample input features and the per-tile compositing (forward,
 // loss, reverse) shared by the fused kernels (lnerf_fused.hip, lnerf_k16.hip). Templates over the
 // kernel's argument struct (fields: input_mode, x, S, k0, near_t, far_t, rays, rpw, dists,
-// target, acc_color, seed, d_target, d_dists). A tile is 128 samples of whole rays; threads
-// 0..127 own one sample each, every other thread of the workgroup only joins the barriers.
+// target, acc_color, seed, d_target, d_dists). A tile is TS samples of whole rays (128 for k16,
+// 256 for the render kernel); threads 0..TS-1 own one sample each, every other thread of the
+// workgroup only joins the barriers.
 #pragma once
 #include "lnerf_internal.h"
 
@@ -10,7 +11,7 @@ namespace lnerf {
 namespace comp {
 
 constexpr int kTileSamples = 128;
-constexpr int kCompFloats = 24;            // per-sample compositing scratch floats in LDS
+constexpr int kCompFloats = 21;            // per-sample compositing scratch floats in LDS (21 TS)
 
 // Coordinate c of sample row gs: the given point (POINTS) or o + d t in float64 (RAYS).
 template <class A>
@@ -35,8 +36,8 @@ __device__ __forceinline__ float input_feature(const A& a, int gs, bool valid, i
     return (fb & 1) ? (float)cos(arg) : (float)sin(arg);
 }
 
-// ---- rendering (nerf.py:176-302), loss and its reverse for one 128-sample tile ----------------
-// One thread per sample (threads 0..127; a ray = S consecutive samples = one scan segment), the
+// ---- rendering (nerf.py:176-302), loss and its reverse for one TS-sample tile -----------------
+// One thread per sample (threads 0..TS-1; a ray = S consecutive samples = one scan segment), the
 // along-ray dependencies as segmented Hillis-Steele scans in LDS (log2 S rounds):
 //   forward  P_j = prod_{i<=j} c_i (inclusive, T_0 = 1, T_j = P_j: nerf.py:226-272),
 //            C = sum_j w_j rgb_j (segmented sum, read at the ray's last sample);
@@ -45,20 +46,21 @@ __device__ __forceinline__ float input_feature(const A& a, int gs, bool valid, i
 // Every per-sample expression is loma's (composite rules of lnerf_generic.hip); only the
 // association of the along-ray products and sums differs from loma's sequential loops, at fp32
 // rounding level (the parity tolerance covers it; the generic path keeps the exact order).
-// LDS: comp[0..512) z [128][4] (in), [512..1024) gz [128][4] (out), two [4][128] ping-pong scan
-// buffers at 1024 / 1536, P at 2048, per-ray dacc [128][4] at 2176 (kCompFloats = 24 per sample).
+// LDS (floats): z [TS][4] at 0 (in), gz [TS][4] at 4 TS (out), two [4][TS] ping-pong scan
+// buffers at 8 TS / 12 TS, P at 16 TS, per-ray dacc [TS][4] at 17 TS (kCompFloats = 21 per sample).
+template <int TS = kTileSamples>
 __device__ __forceinline__ void seg_scan_fwd(float* buf0, float* buf1, int ls, int j, int S, int nv,
                                              float (&v)[4], bool prod_first) {
     // inclusive segmented scan of nv values (v[0] by product if prod_first, the rest by sum)
     float* cur = buf0;
     float* nxt = buf1;
     for (int d = 1; d < S; d <<= 1) {
-        if (ls < kTileSamples)
-            for (int q = 0; q < nv; ++q) cur[q * kTileSamples + ls] = v[q];
+        if (ls < TS)
+            for (int q = 0; q < nv; ++q) cur[q * TS + ls] = v[q];
         __syncthreads();
-        if (ls < kTileSamples && j >= d) {
+        if (ls < TS && j >= d) {
             for (int q = 0; q < nv; ++q) {
-                const float o = cur[q * kTileSamples + ls - d];
+                const float o = cur[q * TS + ls - d];
                 v[q] = (q == 0 && prod_first) ? o * v[q] : o + v[q];
             }
         }
@@ -69,18 +71,18 @@ __device__ __forceinline__ void seg_scan_fwd(float* buf0, float* buf1, int ls, i
     __syncthreads();   // the next scan may write the buffer this one read last
 }
 
-template <class A>
+template <int TS = kTileSamples, class A>
 __device__ __forceinline__ float composite_tile(const A& a, int wg, float* comp, float* rayloss,
                                                 bool grad) {
     const int tid = threadIdx.x, S = a.S;
     float* c_z = comp;
-    float* c_gz = comp + 512;
-    float* sb0 = comp + 1024;
-    float* sb1 = comp + 1536;
-    float* c_P = comp + 2048;
-    float* c_ray = comp + 2176;               // [128 rays][4]: dacc0..2 of each ray
+    float* c_gz = comp + 4 * TS;
+    float* sb0 = comp + 8 * TS;
+    float* sb1 = comp + 12 * TS;
+    float* c_P = comp + 16 * TS;
+    float* c_ray = comp + 17 * TS;            // [TS rays][4]: dacc0..2 of each ray
     const int ntile = a.rpw * S;              // samples of whole rays in this tile
-    const int ls = tid < kTileSamples ? tid : kTileSamples;   // threads >= 128 only sync
+    const int ls = tid < TS ? tid : TS;       // threads >= TS only sync
     const int rl = ls / S, j = ls - rl * S;   // ray within the tile, sample within the ray
     const int ray = wg * a.rpw + rl;
     const bool valid = ls < ntile && ray < a.rays;
@@ -99,14 +101,14 @@ __device__ __forceinline__ float composite_tile(const A& a, int wg, float* comp,
     }
     // P_j (inclusive product), T_j, w_j
     float v[4] = {cc, 0, 0, 0};
-    seg_scan_fwd(sb0, sb1, ls, j, S, 1, v, true);
+    seg_scan_fwd<TS>(sb0, sb1, ls, j, S, 1, v, true);
     const float P = v[0];
     const float T = (j == 0) ? 1.0f : P;
     const float w = al * T;
-    if (ls < kTileSamples) c_P[ls] = P;
+    if (ls < TS) c_P[ls] = P;
     // colour: segmented sum of w * rgb (read at the ray's last sample)
     float cv[4] = {w * rgb[0], w * rgb[1], w * rgb[2], 0};
-    seg_scan_fwd(sb0, sb1, ls, j, S, 3, cv, false);
+    seg_scan_fwd<TS>(sb0, sb1, ls, j, S, 3, cv, false);
     float loss = 0.0f;
     const bool last = valid && j == S - 1;
     if (last) {
@@ -145,7 +147,7 @@ __device__ __forceinline__ float composite_tile(const A& a, int wg, float* comp,
     // G_j = a_j + c_{j+1} G_{j+1}: segmented suffix scan of (a, b) pairs
     float ga = (j >= 1) ? al * dw : 0.0f;
     float gb = 0.0f;
-    if (ls < kTileSamples) sb0[ls] = cc;
+    if (ls < TS) sb0[ls] = cc;
     __syncthreads();
     if (valid && j + 1 < S) gb = sb0[ls + 1];
     __syncthreads();
@@ -153,13 +155,13 @@ __device__ __forceinline__ float composite_tile(const A& a, int wg, float* comp,
         float* cur = sb0;
         float* nxt = sb1;
         for (int d = 1; d < S; d <<= 1) {
-            if (ls < kTileSamples) {
+            if (ls < TS) {
                 cur[ls] = ga;
-                cur[kTileSamples + ls] = gb;
+                cur[TS + ls] = gb;
             }
             __syncthreads();
-            if (ls < kTileSamples && j + d < S) {
-                const float oa = cur[ls + d], ob = cur[kTileSamples + ls + d];
+            if (ls < TS && j + d < S) {
+                const float oa = cur[ls + d], ob = cur[TS + ls + d];
                 ga = ga + gb * oa;
                 gb = gb * ob;
             }
@@ -189,7 +191,7 @@ __device__ __forceinline__ float composite_tile(const A& a, int wg, float* comp,
             }
             c_gz[ls * 4 + k] = g;
         }
-    } else if (ls < kTileSamples) {
+    } else if (ls < TS) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) c_gz[ls * 4 + k] = 0.0f;
     }

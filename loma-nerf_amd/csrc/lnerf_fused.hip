@@ -363,11 +363,31 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
     mark(5);
 }
 
+// Plain bf16 (config 5's inference precision) runs kr (lnerf_render.hip: every weight fragment
+// feeds two 16-sample groups) unless LNERF_RENDER_K16 asks for k16's forward; the split
+// precisions run k16's forward. Both read k16_pack's planes.
+bool fused_render_uses_kr(const FusedPlan& p, int flags) { return !(flags & LNERF_RENDER_K16) && kr_supported(p); }
+
 void fused_render(const FusedPlan& p, const float* ws, const float* bs, const lnerf_batch& b,
-                  const lnerf_outputs& out, hipStream_t s) {
+                  const lnerf_outputs& out, hipStream_t s, int flags, hipEvent_t* ev) {
+    auto mark = [&](int i) {
+        if (ev) (void)hipEventRecord(ev[i], s);
+    };
+    mark(0);
     k16_pack(p, ws, bs, s);
-    k16_launch(p, b, 1.0f, out, false, s);
-    loss_reduce_kernel<<<1, 256, 0, s>>>(p.loss_part, p.num_wg, p.loss_total, out.loss);
+    mark(1);
+    int parts = p.num_wg;
+    if (fused_render_uses_kr(p, flags)) {
+        kr_launch(p, b, out, s);
+        parts = kr_num_wg(p);
+    } else {
+        k16_launch(p, b, 1.0f, out, false, s);
+    }
+    mark(2);
+    loss_reduce_kernel<<<1, 256, 0, s>>>(p.loss_part, parts, p.loss_total, out.loss);
+    mark(3);
+    mark(4);
+    mark(5);
 }
 
 }  // namespace lnerf

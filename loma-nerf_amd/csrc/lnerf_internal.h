@@ -187,8 +187,10 @@ void fused_plan(FusedPlan& p, const lnerf_mlp& mlp, const lnerf_batch& b, void* 
 void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, const lnerf_batch& b,
                       float seed, int flags, const lnerf_outputs& out, hipStream_t s,
                       hipEvent_t* ev);
+// ev: nullable array of events as fused_train_step's ([1]-[2] bracket the forward kernel)
 void fused_render(const FusedPlan& p, const float* ws, const float* bs, const lnerf_batch& b,
-                  const lnerf_outputs& out, hipStream_t s);
+                  const lnerf_outputs& out, hipStream_t s, int flags, hipEvent_t* ev);
+bool fused_render_uses_kr(const FusedPlan& p, int flags);
 void dw16_launch(const FusedPlan& p, hipStream_t s);
 // after a training k1: the batch loss (loss_total, out_loss) and the per-layer dW product shifts,
 // in one launch (lnerf_dw16.hip)
@@ -199,5 +201,9 @@ void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lner
                 bool want_grad, hipStream_t s);
 // the last training k1's ReLU decisions as (L-1, R, 32) bytes (lnerf_ctx_relu_masks)
 void k16_masks_launch(const FusedPlan& p, unsigned char* out, hipStream_t s);
+// kr, the forward-only bf16 render kernel (lnerf_render.hip): two 16-sample groups per wave
+bool kr_supported(const FusedPlan& p);
+int kr_num_wg(const FusedPlan& p);
+void kr_launch(const FusedPlan& p, const lnerf_batch& b, const lnerf_outputs& out, hipStream_t s);
 
 }  // namespace lnerf

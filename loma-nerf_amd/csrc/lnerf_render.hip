@@ -1,0 +1,393 @@
+// lnerf_render.hip -- kr: the forward-only eval render (config 5) on plain bf16 MFMA, with every
+// weight fragment read from LDS feeding two MFMAs.
+//
+// Reference: the eval render of train_nerf.py:558-712 -- get_rays, sampling (:289-306), the
+// positional encoding (pos_encoding.py:38-69), the MLP forward (scripts/nerf.py:67-170) and the
+// compositing (nerf.py:176-302), forward only, at the config-5 inference precision (bf16 operands,
+// fp32 accumulate).
+//
+// Why a kernel of its own: k16 (lnerf_k16.hip) keeps 16 samples per wave and fp32 activations
+// for the training slabs and operand splits; forward-only in one plane, each 16-B fragment read
+// there feeds one 16-cycle MFMA, so the LDS reads (4 array cycles per wave instruction, 256 B/clk
+// per CU) run as long as the matrix core (MI355X_MICROARCH.md §LDS). Here
+//  * a wave owns 32 samples as two 16-sample groups, and every fragment it reads feeds the two
+//    groups' MFMAs: half the LDS bytes per MFMA;
+//  * the activations live only as the next layer's bf16 B operands (8 k-steps x 4 registers per
+//    group), written once per layer by the epilogue in k16's phi order (no data movement between
+//    layers), so the two groups' accumulators (128 registers) fit beside them at two waves per
+//    SIMD;
+//  * one 512-thread workgroup per 256-sample tile of whole rays; the weight stream, its packing
+//    (k16_pack with one plane), the LDS-DMA ring and the chunk table are k16's.
+#include "lnerf_composite.h"
+#include "lnerf_internal.h"
+
+#include <stddef.h>
+
+#include <utility>
+
+namespace lnerf {
+
+namespace {
+
+typedef float fx4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+
+constexpr int kWaves = 8;
+constexpr int kGroups = 2;                       // 16-sample groups per wave
+constexpr int kTile = kWaves * kGroups * 16;     // 256 samples per workgroup
+constexpr int kMaxT = 16;                        // 16-wide output tiles of a 256-wide layer
+constexpr int kKC = 2;                           // k-steps per chunk
+constexpr int kSlot = kKC * kMaxT * 1024;        // one chunk: 2 k-steps x 16 tiles x 1 KiB
+constexpr int kMaxChunks = kMaxLayers * 4 + 1;   // <= 4 chunks per forward pass + the end marker
+constexpr int kOffComp = 2 * kSlot;              // ring: 2 slots
+constexpr int kOffRay = kOffComp + comp::kCompFloats * kTile * 4;
+constexpr int kOffBias = kOffRay + kTile * 4;
+constexpr int kLds = kOffBias + 3 * 256 * 4;     // + a 3-slot ring of layer biases
+static_assert(kLds <= 160 * 1024, "LDS budget");
+constexpr int kPePerWave = 16 * 65 * 4;          // the encoding scratch of one wave (16 samples)
+static_assert(kWaves * kPePerWave <= 2 * kSlot, "the encoding scratch lives in the ring");
+
+struct KrArgs {
+    int L;
+    int ks[kMaxLayers];        // forward k-steps (32 input features) per layer
+    int k0;
+    const unsigned short* w16;
+    const float* b16;          // [L][256] zero-padded biases
+    // the chunk stream: per chunk {u16 offset in w16, (bytes / 1024) | (bias layer + 1) << 16},
+    // zero past the end; read with scalar loads from the kernel-argument segment
+    unsigned chunk_tab[2 * kMaxChunks];
+    int rays, S, rpw, R, input_mode, F;
+    float near_t, far_t;
+    const float* x;
+    const float* dists;
+    const float* target;
+    float* loss_part;
+    float* acc_color;
+    // composite_tile's reverse-pass fields (unused: forward only)
+    float* d_dists;
+    float* d_target;
+    float seed;
+};
+
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+    return (unsigned)(size_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// One LDS-DMA wave instruction from inline asm, M0 written in the same statement (no register
+// destination; completion counted by the chunk barrier's vmcnt). As lnerf_k16.hip glds16.
+__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc),
+                 "s"(__builtin_amdgcn_readfirstlane(lds)));
+}
+
+// feature of k-step s in element j of lane group g (k16's phi: the accumulator layout of the
+// previous layer is the B operand as it stands)
+__host__ __device__ __forceinline__ int phi(int s, int g, int j) {
+    return 32 * s + 16 * (j >> 2) + 4 * g + (j & 3);
+}
+
+struct Chunk {
+    const char* src;   // nullptr: past the last chunk
+    int bytes;
+    int bias;          // layer whose biases ride with this chunk, -1: none
+};
+
+__device__ __forceinline__ Chunk chunk_at(const KrArgs& a, int ci) {
+    const __attribute__((address_space(4))) unsigned* t =
+        (const __attribute__((address_space(4))) unsigned*)((const __attribute__((address_space(4))) char*)
+                                                                __builtin_amdgcn_kernarg_segment_ptr() +
+                                                            offsetof(KrArgs, chunk_tab)) + 2 * ci;
+    const unsigned off = t[0], e = t[1];
+    const int bytes = (int)(e & 0xFFFFu) * 1024;
+    return Chunk{bytes ? (const char*)(a.w16 + off) : nullptr, bytes, (int)(e >> 16) - 1};
+}
+
+// This wave's pieces of a chunk (1 KiB each, at byte wave * 1 KiB + p * 8 KiB), plus the bias
+// piece from the last wave.
+struct Job {
+    const char* src = nullptr;
+    unsigned char* dst = nullptr;
+    int n = 0;
+};
+
+__device__ __forceinline__ Job chunk_job(const KrArgs& a, int ci, unsigned char* ring, float* bias_ring) {
+    const Chunk c = chunk_at(a, ci);
+    const int wave = wave_id(), lane = threadIdx.x & 63;
+    Job j;
+    const int woff = wave * 1024;
+    j.n = (c.src && woff < c.bytes) ? (c.bytes - woff + kWaves * 1024 - 1) / (kWaves * 1024) : 0;
+    j.src = c.src + woff + lane * 16;
+    j.dst = ring + (ci & 1) * kSlot + woff;
+    if (c.bias >= 0 && wave == kWaves - 1)
+        glds16(a.b16 + (size_t)c.bias * 256 + lane * 4, lds_addr(bias_ring + (c.bias % 3) * 256));
+    return j;
+}
+
+template <int P>
+__device__ __forceinline__ void job_piece(const Job& j) {
+    if (P < j.n) glds16(j.src + P * (kWaves * 1024), lds_addr(j.dst + P * (kWaves * 1024)));
+}
+
+// the chunk the next k-step reads has landed (every DMA of this wave: vmcnt(0); the pass issues
+// no other vector-memory operation), this wave's LDS reads of the slot the next DMA overwrites have
+// returned (lgkmcnt(0)), then the workgroup barrier
+__device__ __forceinline__ void chunk_barrier() {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ fx4 mfma(const bf8& a, const bf8& b, fx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+constexpr int kDist = 2;   // fragments read ahead of the one the MFMAs consume
+
+// Output tile O of k-step S: read tile O + kDist's fragment, issue this tile's DMA piece (pieces
+// spread one per NTO / pieces tiles), the two groups' MFMAs on tile O's fragment.
+template <int NTO, int O>
+__device__ __forceinline__ void kr_tile(const unsigned char* base, bf8 (&w)[kDist + 1], const bf8& b0, const bf8& b1,
+                                        fx4 (&acc)[kGroups][kMaxT], const Job& job) {
+    if constexpr (O + kDist < NTO) w[(O + kDist) % (kDist + 1)] = *(const bf8*)(base + (O + kDist) * 1024);
+    // 4 pieces per wave for a whole 16-tile chunk: one every 4 tiles; NTO < 16: all at tile 0
+    if constexpr (NTO >= 4) {
+        if constexpr (O % (NTO / 4) == 0) job_piece<O / (NTO / 4)>(job);
+    } else if constexpr (O == 0) {
+        job_piece<0>(job);
+        job_piece<1>(job);
+        job_piece<2>(job);
+        job_piece<3>(job);
+    }
+    const bf8& f = w[O % (kDist + 1)];
+    acc[0][O] = mfma(f, b0, acc[0][O]);
+    acc[1][O] = mfma(f, b1, acc[1][O]);
+}
+
+template <int NTO, int... O>
+__device__ __forceinline__ void kr_tiles(std::integer_sequence<int, O...>, const unsigned char* base,
+                                         bf8 (&w)[kDist + 1], const bf8& b0, const bf8& b1,
+                                         fx4 (&acc)[kGroups][kMaxT], const Job& job) {
+    (kr_tile<NTO, O>(base, w, b0, b1, acc, job), ...);
+}
+
+// k-step S of a pass (S < ks): chunk ci's sub-step S % 2; the first sub-step issues chunk ci + 1's
+// DMA, the last meets the barrier that waits for it.
+template <int NTO, int S>
+__device__ __forceinline__ void kr_step(const KrArgs& a, int ks, int& ci, unsigned char* ring, float* bias_ring,
+                                        const bf8 (&B)[kGroups][8], fx4 (&acc)[kGroups][kMaxT]) {
+    if (S >= ks) return;
+    constexpr int kk = S % kKC;
+    const bool last = kk == kKC - 1 || S + 1 == ks;
+    Job job;
+    if (kk == 0) job = chunk_job(a, ci + 1, ring, bias_ring);
+    const int lane = threadIdx.x & 63;
+    const unsigned char* base = ring + (ci & 1) * kSlot + kk * NTO * 1024 + lane * 16;
+    bf8 w[kDist + 1];
+    w[0] = *(const bf8*)(base);
+    if constexpr (NTO > 1) w[1] = *(const bf8*)(base + 1024);
+    kr_tiles<NTO>(std::make_integer_sequence<int, NTO>{}, base, w, B[0][S], B[1][S], acc, job);
+    if (last) {
+        chunk_barrier();
+        ++ci;
+    }
+}
+
+template <int NTO, int... S>
+__device__ __forceinline__ void kr_pass(std::integer_sequence<int, S...>, const KrArgs& a, int ks, int& ci,
+                                        unsigned char* ring, float* bias_ring, const bf8 (&B)[kGroups][8],
+                                        fx4 (&acc)[kGroups][kMaxT]) {
+    (kr_step<NTO, S>(a, ks, ci, ring, bias_ring, B, acc), ...);
+}
+
+// Bias + ReLU of a hidden layer's accumulators into the next layer's bf16 B operands: tile o,
+// register i of lane group g is feature 16 o + 4 g + i = phi(o / 2, g, 4 (o % 2) + i), so
+// B[s][j] takes tile 2s + (j >> 2), register j & 3 (nerf.py:98,125 bias after the sum;
+// :141-144 ReLU).
+template <int HT>
+__device__ __forceinline__ void kr_epilogue(const float* bl, const fx4 (&acc)[kGroups][kMaxT], bf8 (&B)[kGroups][8]) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        if (2 * s >= HT) {
+            B[0][s] = bf8{};
+            B[1][s] = bf8{};
+            continue;
+        }
+        const fx4 b0 = *(const fx4*)(bl + 32 * s);
+        const fx4 b1 = *(const fx4*)(bl + 32 * s + 16);
+#pragma unroll
+        for (int G = 0; G < kGroups; ++G) {
+            bf8 v;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float x0 = acc[G][2 * s][i] + b0[i];
+                const float x1 = acc[G][2 * s + 1][i] + b1[i];
+                v[i] = (__bf16)(x0 > 0.0f ? x0 : 0.0f);
+                v[4 + i] = (__bf16)(x1 > 0.0f ? x1 : 0.0f);
+            }
+            B[G][s] = v;
+        }
+    }
+}
+
+template <int HT>
+__global__ void __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(2, 2)))
+kr_fwd_kernel(KrArgs a) {
+    __shared__ __attribute__((aligned(16))) unsigned char lds[kLds];
+    unsigned char* ring = lds;
+    float* comp = (float*)(lds + kOffComp);
+    float* rayloss = (float*)(lds + kOffRay);
+    float* bias_ring = (float*)(lds + kOffBias);
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id(), g = lane >> 4, n = lane & 15;
+    const int wg = blockIdx.x;
+    const int tile_samples = a.rpw * a.S;
+
+    // ---- layer-0 input (k0 <= 64: two k-steps) as bf16 B operands, group by group, through a
+    // per-wave LDS scratch [16 samples][65]: POINTS / RAYS encode with one float64 sincos per
+    // (sample, coordinate, frequency) (pos_encoding.py:54-66), ENCODED copies loma's layer_input
+    bf8 B[kGroups][8];
+#pragma unroll
+    for (int G = 0; G < kGroups; ++G) {
+        constexpr int kStride = 65;
+        float* pe = (float*)ring + wave * (16 * kStride);
+        const int lbase = wave * 32 + G * 16;                 // local sample of the group's row 0
+        const int tile_base = wg * tile_samples + lbase;
+        if (a.input_mode != LNERF_INPUT_ENCODED) {
+            const int F = a.F, per = 3 * (F + 1);
+            for (int it = lane; it < 16 * per; it += 64) {
+                const int sl = it / per, rem = it - sl * per, c = rem % 3, q = rem / 3;
+                const bool vs = (lbase + sl < tile_samples) && (tile_base + sl < a.R);
+                const double xc = vs ? comp::sample_coord(a, tile_base + sl, c) : 0.0;
+                if (q == 0) {
+                    pe[sl * kStride + c] = (float)xc;
+                } else {
+                    double sn, cs;
+                    sincos(ldexp(xc, q - 1), &sn, &cs);
+                    pe[sl * kStride + 3 + 6 * (q - 1) + c] = (float)sn;
+                    pe[sl * kStride + 6 + 6 * (q - 1) + c] = (float)cs;
+                }
+            }
+            for (int e = lane; e < 16 * 64; e += 64) {
+                const int sl = e >> 6, f = e & 63;
+                if (f >= a.k0) pe[sl * kStride + f] = 0.0f;
+            }
+        } else {
+            for (int e = lane; e < 16 * 64; e += 64) {
+                const int sl = e >> 6, f = e & 63;
+                const bool vs = (lbase + sl < tile_samples) && (tile_base + sl < a.R) && f < a.k0;
+                pe[sl * kStride + f] = vs ? a.x[(size_t)(tile_base + sl) * a.k0 + f] : 0.0f;
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            bf8 v = {};
+            if (s < 2)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = (__bf16)pe[n * kStride + phi(s, g, j)];
+            B[G][s] = v;
+        }
+    }
+    __syncthreads();   // the first DMA overwrites the scratch
+
+    int ci = 0;
+    {
+        const Job j0 = chunk_job(a, 0, ring, bias_ring);
+        job_piece<0>(j0);
+        job_piece<1>(j0);
+        job_piece<2>(j0);
+        job_piece<3>(j0);
+        chunk_barrier();
+    }
+
+    fx4 acc[kGroups][kMaxT];
+    for (int l = 0; l < a.L; ++l) {
+        const float* bl = bias_ring + (l % 3) * 256 + g * 4;
+        const int ks = a.ks[l];
+#pragma unroll
+        for (int G = 0; G < kGroups; ++G)
+#pragma unroll
+            for (int o = 0; o < kMaxT; ++o) acc[G][o] = fx4{0.0f, 0.0f, 0.0f, 0.0f};
+        if (l < a.L - 1) {
+            kr_pass<HT>(std::make_integer_sequence<int, 8>{}, a, ks, ci, ring, bias_ring, B, acc);
+            kr_epilogue<HT>(bl, acc, B);
+        } else {
+            kr_pass<1>(std::make_integer_sequence<int, 8>{}, a, ks, ci, ring, bias_ring, B, acc);
+            // head pre-activations (features 0..3: registers 0..3 of lane group 0), after the sum
+            if (g == 0) {
+                const fx4 b = *(const fx4*)bl;
+#pragma unroll
+                for (int G = 0; G < kGroups; ++G) {
+                    const int ls = wave * 32 + G * 16 + n;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) comp[ls * 4 + i] = acc[G][0][i] + b[i];
+                }
+            }
+        }
+    }
+    __syncthreads();
+    comp::composite_tile<kTile>(a, wg, comp, rayloss, false);
+    __syncthreads();
+    if (tid == 0) {
+        float lsum = 0.0f;
+        for (int r = 0; r < a.rpw; ++r) lsum = lsum + rayloss[r];
+        a.loss_part[wg] = lsum;
+    }
+}
+
+}  // namespace
+
+// plain bf16, the NeRF head, whole rays of <= 128 samples, a layer-0 input of <= 64 features
+// (PE with F <= 10); anything else renders on k16's forward
+bool kr_supported(const FusedPlan& p) {
+    return p.x6 == 1 && !p.head_fit && p.S <= 128 && p.n[p.L - 1] <= 16 && p.tile == 128 && p.k[0] <= 64;
+}
+
+int kr_num_wg(const FusedPlan& p) {
+    const int rpw = kTile / p.S;
+    return (p.rays + rpw - 1) / rpw;
+}
+
+void kr_launch(const FusedPlan& p, const lnerf_batch& b, const lnerf_outputs& out, hipStream_t s) {
+    KrArgs a{};
+    a.L = p.L;
+    for (int l = 0; l < p.L; ++l) a.ks[l] = p.ks16_f[l];
+    a.k0 = p.k[0];
+    a.w16 = p.w16;
+    a.b16 = p.b16;
+    a.rays = p.rays;
+    a.S = p.S;
+    a.rpw = kTile / p.S;
+    a.R = p.R;
+    a.input_mode = b.input_mode;
+    a.F = b.num_freqs;
+    a.near_t = b.near_t;
+    a.far_t = b.far_t;
+    a.x = b.x;
+    a.dists = b.input_mode == LNERF_INPUT_RAYS ? nullptr : b.dists;
+    a.target = b.target;
+    a.loss_part = p.loss_part;
+    a.acc_color = out.acc_color;
+    a.seed = 1.0f;
+    // the forward chunk stream of k16_pack's one-plane packing: 2 k-steps per chunk
+    int ci = 0;
+    for (int l = 0; l < p.L; ++l) {
+        const size_t per = (size_t)p.to16_f[l] * 512;   // u16 per k-step
+        for (int s2 = 0; s2 < p.ks16_f[l]; s2 += kKC, ++ci) {
+            const int nk = p.ks16_f[l] - s2 < kKC ? p.ks16_f[l] - s2 : kKC;
+            a.chunk_tab[2 * ci] = (unsigned)(p.w16f_off[l] + (size_t)s2 * per);
+            a.chunk_tab[2 * ci + 1] = (unsigned)(nk * per * 2 / 1024) | ((s2 == 0 ? l + 1 : 0) << 16);
+        }
+    }
+    static_assert(sizeof(KrArgs) <= 4096, "kernel arguments");
+    const int grid = kr_num_wg(p);
+    switch (p.ht16) {
+        case 1: kr_fwd_kernel<1><<<grid, 64 * kWaves, 0, s>>>(a); break;
+        case 2: kr_fwd_kernel<2><<<grid, 64 * kWaves, 0, s>>>(a); break;
+        case 4: kr_fwd_kernel<4><<<grid, 64 * kWaves, 0, s>>>(a); break;
+        case 8: kr_fwd_kernel<8><<<grid, 64 * kWaves, 0, s>>>(a); break;
+        default: kr_fwd_kernel<16><<<grid, 64 * kWaves, 0, s>>>(a); break;
+    }
+}
+
+}  // namespace lnerf

@@ -29,3 +29,22 @@ def allreduce_loss_seeded(packed, dist, scale_fn=None, group=None):
     else:
         scale_fn(grads, loss)
     return packed
+
+
+def gather_rows(local, n_total, dist, group=None):
+    """Config 5's final gather ("replicas only, then a final gather of 640 000 x 3
+    colours"): every rank holds the rows [lo, hi) of its dp.shard_rays range; returns the whole
+    (n_total, ...) array on every rank. Shards differ by at most one row, so each is padded to
+    ceil(n_total / world) rows for one all_gather and the padding is dropped in rank order."""
+    import torch
+    world = dist.get_world_size(group)
+    chunk = -(-n_total // world)
+    pad = torch.zeros((chunk,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    pad[: local.shape[0]] = local
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad, group=group)
+    rows = []
+    for r in range(world):
+        lo, hi = shard_rays(n_total, world, r)
+        rows.append(parts[r][: hi - lo])
+    return torch.cat(rows, 0)

@@ -36,6 +36,7 @@ ONE_WAVE = 1024    # removed in round 4 (the one-wave-per-SIMD kernel pair): an 
 K32 = 2048         # removed in round 4 (k32 lost to k16): an error
 K16_W4 = 4096      # fused path: k16 on 4-wave 64-sample workgroups, two per CU (A/B)
 HEAD_FIT = 8192    # the mlp_fit head (sigmoid on every output, no compositing; samples = 1)
+RENDER_K16 = 16384  # render (plain bf16) on k16's forward instead of kr (A/B)
 
 OPT_DW_GRID = 1    # lnerf_ctx_set_option: dW workgroups per step (0 = default 512)
 
@@ -55,6 +56,7 @@ PATH_K16 = 4
 PATH_DW16 = 8
 PATH_K32 = 16      # reserved (k32, removed in round 4)
 PATH_K16_W4 = 32
+PATH_KR = 64       # the render ran kr (lnerf_render.hip)
 
 
 class LnerfMLP(ctypes.Structure):
@@ -339,6 +341,7 @@ class Engine:
             raise RuntimeError(f"lnerf_ctx_last_path: {last_error()}")
         return dict(generic=bool(v & PATH_GENERIC), fused=bool(v & PATH_FUSED),
                     k16=bool(v & PATH_K16), dw16=bool(v & PATH_DW16), k16_w4=bool(v & PATH_K16_W4),
+                    kr=bool(v & PATH_KR),
                     planes=(v >> 8) & 3)
 
     def relu_masks(self, L: int, R: int):

@@ -25,3 +25,10 @@ if [ -f $L/libloma_nerf_r3ilp.so ]; then
 fi
 bash scripts/gpu_ab.sh $L/libloma_nerf.so $L/libloma_nerf_r3.so $L/libloma_nerf_ilp.so \
   $L/libloma_nerf.so $L/libloma_nerf_r3.so $L/libloma_nerf_ilp.so
+# the config-5 render: kr (default) vs k16's bf16 forward, interleaved
+for i in 1 2; do
+  for v in "" "--render-k16"; do
+    timeout -k 10 120 python bench.py --render --steps 5 --warmup 2 $v > gpurun_out/render_ab.log 2>&1 || { echo "render $v failed"; tail -5 gpurun_out/render_ab.log; exit 1; }
+    python -c "import json;d=json.loads([l for l in open('gpurun_out/render_ab.log') if l.startswith('{')][-1]);r=d['roofline'];print('render ${v:-kr}', round(d['ms_per_step'],2), 'ms/frame', r['kernel'], 'kernel', round(r.get('avg_ms',0),2), 'ms frac', round(r['frac'],3))"
+  done
+done

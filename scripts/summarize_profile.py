@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Turns a scripts/gpu_profile.sh run (gpurun_out/prof/) into the committed summaries under
+"""Turns a scripts/gpu_steps.sh trace + pmc run (gpurun_out/prof/ or rprof/) into the committed summaries under
 profiles/:
 
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied as is)
@@ -9,9 +9,11 @@ profiles/:
                                     half the bytes of 16 B/lane streaming reads -> x2;
                                     WRITE_SIZE is exact for 16 B/lane stores. Both are in KiB.
 
-bench.py reads <tag>_pmc.json (newest tag) to fill roofline.traffic for the same workload.
+bench.py reads <tag>_pmc.json (newest tag whose lib_sha16 is the loaded library's) to fill
+roofline.traffic for the same workload. The library hash is the one the GPU step recorded next to
+the traces (<src>/lib_sha16.txt, scripts/gpu_steps.sh).
 
-    python scripts/summarize_profile.py r01 [gpurun_out/prof]
+    python scripts/summarize_profile.py r04 [gpurun_out/prof] [--workload cfg3|cfg5] [--name r04_render]
 """
 import collections
 import csv
@@ -37,12 +39,19 @@ def per_kernel(path):
 
 
 def main():
-    tag = sys.argv[1]
-    src = sys.argv[2] if len(sys.argv) > 2 else os.path.join(REPO, "gpurun_out", "prof")
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("src", nargs="?", default=os.path.join(REPO, "gpurun_out", "prof"))
+    ap.add_argument("--workload", default="cfg3")
+    ap.add_argument("--name", default=None, help="output file stem (default: the tag)")
+    a = ap.parse_args()
+    tag, src = a.tag, a.src
+    name = a.name or tag
     dst = os.path.join(REPO, "profiles")
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
-                os.path.join(dst, f"{tag}_kernel_stats.csv"))
+                os.path.join(dst, f"{name}_kernel_stats.csv"))
     stats = {}
     for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
         stats[short(r["Name"])] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6}
@@ -50,19 +59,20 @@ def main():
     write = per_kernel(os.path.join(src, "write", "run_counter_collection.csv"))
     kernels = {}
     for k in sorted(set(fetch) | set(write)):
-        if not k.startswith(("fused", "k16", "dw", "grad_reduce", "loss_reduce", "pack", "wmax16", "slab_max", "k32")):
+        if not k.startswith(("k16", "dw", "grad_reduce", "loss_reduce", "pack", "wmax16", "k1_reduce", "adam")):
             continue
         f = fetch.get(k, 0.0) * 1024
         w = write.get(k, 0.0) * 1024
         kernels[k] = {"fetch_size_kib": fetch.get(k), "write_size_kib": write.get(k),
                       "hbm_read_bytes": 2 * f, "hbm_write_bytes": w,
                       "hbm_bytes_per_launch": 2 * f + w, **stats.get(k, {})}
-    cmd = open(os.path.join(HERE, "gpu_profile.sh")).read()
-    args = [l for l in cmd.splitlines() if l.startswith("ARGS=")]
-    out = {"tag": tag, "command": "python3 bench.py " + (args[0][6:-1] if args else ""),
-           "workload": "cfg3", "correction": "hbm_read = 2 x FETCH_SIZE (gfx950), write = WRITE_SIZE",
+    cmdf = os.path.join(src, "command.txt")
+    shaf = os.path.join(src, "lib_sha16.txt")
+    out = {"tag": tag, "command": open(cmdf).read().strip() if os.path.exists(cmdf) else None,
+           "workload": a.workload, "lib_sha16": open(shaf).read().strip() if os.path.exists(shaf) else None,
+           "correction": "hbm_read = 2 x FETCH_SIZE (gfx950), write = WRITE_SIZE",
            "kernels": kernels}
-    with open(os.path.join(dst, f"{tag}_pmc.json"), "w") as fh:
+    with open(os.path.join(dst, f"{name}_pmc.json"), "w") as fh:
         json.dump(out, fh, indent=1)
     for k, v in kernels.items():
         print(f"{k:32s} {v.get('avg_ms', 0):8.3f} ms  read {v['hbm_read_bytes'] / 1e9:7.3f} GB  "

@@ -15,7 +15,9 @@ Derived (MI355X_MICROARCH.md, "rocprofv3 PMC slots", "DVFS give-back", "LDS"):
                       (disjoint, they add up to ~1); SQ_WAIT_INST_LDS is the LDS-issue-stall share
   * per_wave        = SQ_INSTS_* / SQ_WAVES (instruction mix of one wave)
 
-    python scripts/summarize_sq.py r03 [gpurun_out/sq] [profiles/r03_kernel_stats.csv]
+    python scripts/summarize_sq.py r04 [gpurun_out/sq] [profiles/r04_kernel_stats.csv]
+        [--workload cfg3|cfg5] [--name r04_render]
+The library hash comes from <src>/lib_sha16.txt (written by scripts/gpu_sq.sh on the box).
 """
 import collections
 import csv
@@ -26,8 +28,8 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-KEEP = ("k16_fwd_bwd_kernel", "dw16_kernel", "k32_fwd_bwd_kernel", "fused_fwd_bwd_kernel",
-        "grad_reduce_kernel", "k1_reduce_kernel", "pack16_kernel", "adam_kernel")
+KEEP = ("k16_fwd_bwd_kernel", "dw16_kernel", "grad_reduce_kernel", "k1_reduce_kernel", "pack16_kernel",
+        "adam_kernel", "loss_reduce_kernel")
 
 
 def short(name):
@@ -36,9 +38,16 @@ def short(name):
 
 
 def main():
-    tag = sys.argv[1]
-    src = sys.argv[2] if len(sys.argv) > 2 else os.path.join(REPO, "gpurun_out", "sq")
-    stats_csv = sys.argv[3] if len(sys.argv) > 3 else None
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("src", nargs="?", default=os.path.join(REPO, "gpurun_out", "sq"))
+    ap.add_argument("stats_csv", nargs="?", default=None)
+    ap.add_argument("--workload", default="cfg3")
+    ap.add_argument("--name", default=None)
+    a = ap.parse_args()
+    tag, src, stats_csv = a.tag, a.src, a.stats_csv
+    name = a.name or tag
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in sorted(glob.glob(os.path.join(src, "p*", "**", "*counter_collection.csv"), recursive=True)):
         per = collections.defaultdict(float)   # (kernel, dispatch, counter) -> summed over dims
@@ -53,8 +62,13 @@ def main():
     if stats_csv and os.path.exists(stats_csv):
         for r in csv.DictReader(open(stats_csv)):
             dur[short(r["Name"])] = float(r["AverageNs"]) * 1e-9
-    out = {"tag": tag, "source": "scripts/gpu_sq.sh (3 rocprofv3 --pmc passes of bench.py --steps 3 "
-                                 "--warmup 1), per-dispatch averages", "kernels": {}}
+    shaf = os.path.join(src, "lib_sha16.txt")
+    cmdf = os.path.join(src, "command.txt")
+    out = {"tag": tag, "workload": a.workload,
+           "lib_sha16": open(shaf).read().strip() if os.path.exists(shaf) else None,
+           "source": "scripts/gpu_sq.sh (3 rocprofv3 --pmc passes of "
+                     + (open(cmdf).read().strip() if os.path.exists(cmdf) else "bench.py") + "), per-dispatch averages",
+           "kernels": {}}
     for k, cs in sorted(vals.items()):
         avg = {c: sum(v) / len(v) for c, v in cs.items()}
         d = {"dispatches": max(len(v) for v in cs.values()), "counters": avg}
@@ -73,6 +87,8 @@ def main():
             der["lds_conflict"] = avg.get("SQ_LDS_BANK_CONFLICT", 0.0) / avg["SQ_LDS_IDX_ACTIVE"]
         if "SQ_INSTS_VALU_MFMA_MOPS_F16" in avg:
             der["mfma_f16_flops"] = avg["SQ_INSTS_VALU_MFMA_MOPS_F16"] * 512
+        if "SQ_INSTS_VALU_MFMA_MOPS_BF16" in avg:
+            der["mfma_bf16_flops"] = avg["SQ_INSTS_VALU_MFMA_MOPS_BF16"] * 512
         wc = avg.get("SQ_WAVE_CYCLES")
         if wc:
             for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS",
@@ -87,7 +103,7 @@ def main():
         d["derived"] = der
         out["kernels"][k] = d
     os.makedirs(os.path.join(REPO, "profiles"), exist_ok=True)
-    path = os.path.join(REPO, "profiles", f"{tag}_sq.json")
+    path = os.path.join(REPO, "profiles", f"{name}_sq.json")
     with open(path, "w") as fh:
         json.dump(out, fh, indent=1)
     for k, d in out["kernels"].items():

@@ -123,3 +123,37 @@ def test_strong_scaling_shards_cover_one_batch():
         assert sum(p["N"] for p in parts) == b["N"] and all(p["N_total"] == b["N"] for p in parts)
         for k in ("pts", "dists", "rays", "target"):
             assert np.array_equal(np.concatenate([p[k] for p in parts]), b[k]), k
+
+
+def _gather_worker(rank, world, port, n, out):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "loma-nerf_amd"))
+    import dp
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    frame = torch.arange(n * 3, dtype=torch.float32).reshape(n, 3)
+    lo, hi = dp.shard_rays(n, world, rank)
+    got = dp.gather_rows(frame[lo:hi].clone(), n, dist)
+    out.put((rank, bool(torch.equal(got, frame))))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_render_frame_gather_uneven_shards():
+    """bench.py --render at N > 1 (config 5): each rank renders its dp.shard_rays share of the frame
+    and dp.gather_rows reassembles the whole frame in ray order on every rank (train_nerf.py:659-681
+    assembles the eval image), shards of unequal length included (7 rows over 3 ranks)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world, n = 3, 7
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert all(res[r] for r in range(world)), res

@@ -37,6 +37,7 @@ sys.path.insert(0, os.path.join(ROOT, "scripts"))
 K16 = r"k16_fwd_bwd_kernelILi(16|2|4)ELi[123]ELi[48]E"
 K16_SPLIT_BF16 = r"k16_fwd_bwd_kernelILi(16|2|4)ELi[12]ELi[48]E"   # the MFMA rules: fp16x3 + bf16
 DW16 = r"dw16_kernel"
+KR = r"kr_fwd_kernel"   # the bf16 render kernel (lnerf_render.hip)
 OTHER = r"(pack16|wmax16|k16_masks|k1_reduce|grad_reduce|loss_reduce|lg_|k_adam|adam|get_rays|positional|ray_)"
 
 
@@ -62,7 +63,7 @@ def _fmt(name, fs):
 
 def test_every_load_waited_for_before_use(asm):
     bad = []
-    for rx in (K16, DW16, OTHER):
+    for rx in (K16, DW16, KR, OTHER):
         for name, fs in _report(asm, rx).items():
             bad += _fmt(name, [f for f in fs if f[0] == "pending-load"])
     assert not bad, "\n".join(bad)
@@ -70,7 +71,7 @@ def test_every_load_waited_for_before_use(asm):
 
 def test_mfma_wait_states_product_kernels(asm):
     bad = []
-    for rx in (K16_SPLIT_BF16, DW16):
+    for rx in (K16_SPLIT_BF16, DW16, KR):
         for name, fs in _report(asm, rx).items():
             bad += _fmt(name, fs)
     assert not bad, "\n".join(bad)
@@ -78,7 +79,7 @@ def test_mfma_wait_states_product_kernels(asm):
 
 def test_m0_read_only_by_lds_dma(asm):
     import isa_check
-    kernels = isa_check.parse_kernels(asm, K16)
+    kernels = isa_check.parse_kernels(asm, K16 + "|" + KR)
     assert kernels
     bad = []
     for name, insts in kernels.items():

@@ -140,8 +140,12 @@ enum {
                                  MFMAs per product, fp32 accumulate. Each product drops
                                  <= ~3 2^-22 of its operands' shifted magnitudes, i.e. relative to
                                  max|w| max|x| of the shift group (one sample's row of one layer),
-                                 not to |w x| itself (values far below their row's maximum lose
-                                 bits to fp16's subnormal range).                               */
+                                 not to |w x| itself: an operand x scaled by 2^e keeps
+                                 |x 2^e - hi - lo| <= 2^-22 |x 2^e| + 2^-25, so a value more than
+                                 ~2^17 below its row's maximum loses bits to fp16's subnormals
+                                 (e.g. a dW column whose G values sit 1e-9 below the row's other
+                                 columns keeps ~2 % -- tests/test_gpu_edge.py fp16x3_dw_bound;
+                                 LNERF_MFMA_BF16X6 has fp32's exponent range and no such limit). */
     LNERF_MFMA_BF16X6 = 512,  /* fused path: the bf16x6 split (x = hi+mid+lo in bf16, six bf16
                                  MFMAs per product, dropped terms <= 2^-24 |w x|)              */
     LNERF_K32 = 2048,         /* removed in round 4 (it lost to k16): an error                 */

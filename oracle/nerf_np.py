@@ -203,7 +203,8 @@ def nerf_forward_backward(X, ws, bs, dists, target, S, seed=1.0, masks=None):
     per hidden layer l a bool (R, n_l) array of ReLU decisions to use instead of z > 0 in both
     passes (nerf.py:141-144) -- the derivative at another implementation's decisions, for
     comparing with it on rays whose pre-activations sit at |z| ~ 0 (ReLU ties). Also returns the
-    hidden pre-activations Z[l] and their term magnitudes T[l] = |A||W| + |b|."""
+    hidden pre-activations Z[l] and their term magnitudes T[l] = |A||W| + |b|, and the operands of
+    every weight adjoint: A[l] (layer l's input, X for l = 0) and G[l] = dL/dZ_l, dW[l] = A^T G."""
     X = np.asarray(X, np.float64)
     L = len(ws)
     A = [X]
@@ -257,9 +258,11 @@ def nerf_forward_backward(X, ws, bs, dists, target, S, seed=1.0, masks=None):
     dz[:, 3] = np.where(zl[:, 3] > 0, gsigma.reshape(-1), 0.0)
     dW = [None] * L
     db = [None] * L
+    G = [None] * L
     g = dz
     dX = None
     for l in range(L - 1, -1, -1):
+        G[l] = g
         dW[l] = A[l].T @ g
         db[l] = g.sum(0)
         ga = g @ np.asarray(ws[l], np.float64).T
@@ -269,7 +272,7 @@ def nerf_forward_backward(X, ws, bs, dists, target, S, seed=1.0, masks=None):
         else:
             dX = ga
     return dict(loss=loss, acc=C, dW=dW, db=db, dX=dX, d_dists=gdist, d_target=-gC,
-                rgb=rgb, sigma=sg, weights=w, alpha=alpha, Z=Z[:-1], T=Tm)
+                rgb=rgb, sigma=sg, weights=w, alpha=alpha, Z=Z[:-1], T=Tm, A=A, G=G)
 
 
 def nerf_forward_backward_chunked(X, ws, bs, dists, target, S, seed, masks=None, rays_per_chunk=256):

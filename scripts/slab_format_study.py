@@ -86,51 +86,10 @@ FORMATS = {"fp32": lambda x: x, "top24": q_top24, "hi16+e5m2": q_hi16_e5m2, "hi1
 
 def slabs(X, ws, bs, dists, target, S, seed=1.0):
     """A_{l-1} (layer inputs, X for l = 0) and G_l = dL/dZ_l of every layer, float64, from
-    nerf_np.nerf_forward_backward's own recurrences (scripts/nerf.py:1-304 and its rev_diff)."""
+    nerf_np.nerf_forward_backward (scripts/nerf.py:1-304 and its rev_diff)."""
     import nerf_np
     r = nerf_np.nerf_forward_backward(X, ws, bs, dists, target, S, seed=seed)
-    L = len(ws)
-    A = [np.asarray(X, np.float64)] + [np.where(z > 0, z, 0.0) for z in r["Z"]]
-    # G_L-1 from the head, then back through the layers (the same recurrence as nerf_np)
-    zl = A[-1] @ np.asarray(ws[-1], np.float64) + np.asarray(bs[-1], np.float64)[None, :]
-    G = [None] * L
-    # recover dz of the head from dW_L-1 = A^T dz: recompute it directly
-    N = X.shape[0] // S
-    sig = 1.0 / (1.0 + np.exp(-zl[:, :3]))
-    sg = np.where(zl[:, 3] > 0, zl[:, 3], 0.0).reshape(N, S)
-    dl = np.asarray(dists, np.float64).reshape(N, S)
-    e = np.exp(-sg * dl)
-    alpha = 1.0 - e
-    c = (1.0 - alpha) + 1e-10
-    P = np.cumprod(c, axis=1)
-    T = P.copy()
-    T[:, 0] = 1.0
-    w = alpha * T
-    rgb = sig.reshape(N, S, 3)
-    C = (w[:, :, None] * rgb).sum(1)
-    gC = 2.0 * seed * (C - np.asarray(target, np.float64))
-    gw = (gC[:, None, :] * rgb).sum(2)
-    grgb = w[:, :, None] * gC[:, None, :]
-    dP = alpha * gw
-    dP[:, 0] = 0.0
-    dc = np.zeros_like(c)
-    for j in range(S - 1, 0, -1):
-        dP[:, j - 1] += dP[:, j] * c[:, j]
-        dc[:, j] += dP[:, j] * P[:, j - 1]
-    dc[:, 0] += dP[:, 0]
-    galpha = T * gw - dc
-    gsigma = galpha * e * dl
-    dz = np.zeros_like(zl)
-    s3 = sig.reshape(-1, 3)
-    dz[:, :3] = grgb.reshape(-1, 3) * s3 * (1.0 - s3)
-    dz[:, 3] = np.where(zl[:, 3] > 0, gsigma.reshape(-1), 0.0)
-    g = dz
-    for l in range(L - 1, -1, -1):
-        G[l] = g
-        if l > 0:
-            ga = g @ np.asarray(ws[l], np.float64).T
-            g = np.where(A[l] > 0, ga, 0.0)
-    return A[:L], G
+    return r["A"], r["G"]
 
 
 def study(name, X, ws, bs, dists, target, S):

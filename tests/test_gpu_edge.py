@@ -20,11 +20,41 @@ pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PRECS = {"fp16x3": 0, "bf16x6": 512, "generic": 8}
-# fp16x3 dW, per column: |err| <= 1e-4 x the column's own max (the bar of
-# test_gpu_native.py::test_full_size_all_rays_float64); the layer-relative bound below is the
-# documented one (include/lnerf.h, LNERF_MFMA_F16X3), the per-column one is what k2's per-sample
-# balanced shifts deliver on these fixtures (lnerf_dw16.hip sample_shifts)
+# fp16x3 dW per element: |err| <= 1e-5 |want| + 1e-4 x the column's own max (the bar of
+# test_gpu_native.py::test_full_size_all_rays_float64) + 2 x the split's a-priori bound
+# (fp16x3_dw_bound). The bound is what include/lnerf.h (LNERF_MFMA_F16X3) documents: the split
+# keeps 22 bits relative to the operand's own magnitude only while the shifted value stays in
+# fp16's normal range -- an element more than ~2^17 below its row's maximum falls into the
+# subnormals (quantum 2^-24 of the row scale). The edge fixture has exactly that: a G_l column at
+# 1e-9 beside a 0.49 column in the same rows (the delta = 1e8 rays), which loses ~2 % of that
+# column -- inside the bound, not inside the 1e-4 column bar.
 F16X3_COL_TOL = 1e-4
+
+
+def fp16x3_dw_bound(A, G):
+    """Per-element a-priori bound of k2's fp16x3 dW error (lnerf_dw16.hip): every operand x is
+    scaled by 2^e (k1's row shift fp16x3_shift, balanced per sample by sample_shifts) and split
+    as hi + lo in fp16, so |x 2^e - hi - lo| <= 2^-22 |x 2^e| + 2^-25 (half fp16's subnormal
+    quantum); the dropped lo x lo term adds <= 2^-22 |x 2^e| |y 2^f|. Summed over the samples:
+    3 2^-22 sum |A||G| + sum_s |A[s,k]| 2^-25-eg_s [G != 0] + |G[s,n]| 2^-25-ea_s [A != 0]."""
+    def row_shift(x):
+        m = np.abs(x).max(axis=1)
+        e = np.zeros(len(m), np.int64)
+        ok = (m > 0) & np.isfinite(m)
+        e[ok] = np.minimum(14 - np.frexp(m[ok])[1], 127)
+        return e, ~ok
+    A = np.nan_to_num(np.abs(np.asarray(A, np.float64)))
+    G = np.nan_to_num(np.abs(np.asarray(G, np.float64)))
+    xa, za = row_shift(A.astype(np.float32))
+    xg, zg = row_shift(G.astype(np.float32))
+    live = ~(za | zg)
+    E = int((xa + xg)[live].min()) if live.any() else 0
+    d = xa + xg - E
+    ea = np.where(live, xa - (d >> 1), np.where(za, 0, xa))
+    eg = np.where(live, xg - ((d + 1) >> 1), np.where(zg, 0, xg))
+    qa = np.ldexp(1.0, -25 - ea)[:, None]
+    qg = np.ldexp(1.0, -25 - eg)[:, None]
+    return 3 * 2.0 ** -22 * (A.T @ G) + A.T @ (qg * (G > 0)) + (qa * (A > 0)).T @ G
 
 
 def load(name):
@@ -82,19 +112,35 @@ def test_edge_numerics(engine, name, prec):
     close_grouped("d_dists", got["d_dists"], g["d_dists"])
     if prec == "fp16x3":
         # the fp16x3 products keep 22 bits relative to their shift group (one sample's A row and
-        # G row, balanced per sample by k2), so the bound is checked twice: layer-relative as
-        # documented, and per column against F16X3_COL_TOL -- the sigma column (dsigma ~ 1e8 on the
-        # delta = 1e8 rays) dominates its layer's max, so the layer bound alone would leave the
-        # other columns unchecked.
+        # G row, balanced per sample by k2): checked layer-relative as documented, then per element
+        # against the column bar plus the split's a-priori bound (fp16x3_dw_bound) -- the sigma
+        # column (dsigma ~ 1e8 on the delta = 1e8 rays) dominates its layer's max, so the layer
+        # bound alone would leave the other columns unchecked.
         close_grouped("dW", got["dW"].reshape(g["dW"].shape[0], -1), g["dW"].reshape(g["dW"].shape[0], -1),
                       gtol=2e-6)
-        w = np.where(np.isnan(g["dW"]), 0, g["dW"])
-        e = np.abs(np.where(np.isnan(g["dW"]), 0, got["dW"] - w)).max(axis=1)
-        cm = np.abs(w).max(axis=1)
-        worst = float((e[cm > 0] / cm[cm > 0]).max())
-        print(f"{name} fp16x3 worst per-column dW error / column max: {worst:.3g}")
-        assert worst <= F16X3_COL_TOL, worst
-        close_grouped("dW", got["dW"], g["dW"], rtol=1e-5, gtol=F16X3_COL_TOL)
+        import nerf_np
+        shapes = [tuple(int(v) for v in s) for s in g["shapes"]]
+        with np.errstate(all="ignore"):
+            r = nerf_np.nerf_forward_backward(
+                g["X"], [g["wp"][l, :k, :n] for l, (k, n) in enumerate(shapes)],
+                [g["bp"][l, :n] for l, (_, n) in enumerate(shapes)], g["dists"], g["target"], int(g["S"]))
+        worst_col, worst_bound = 0.0, 0.0
+        for l, (k, n) in enumerate(shapes):
+            want = g["dW"][l, :k, :n].astype(np.float64)
+            fin = ~np.isnan(want)
+            w = np.where(fin, want, 0.0)
+            err = np.abs(np.where(fin, got["dW"][l, :k, :n] - w, 0.0))
+            cm = np.abs(w).max(axis=0, keepdims=True)
+            with np.errstate(all="ignore"):
+                bound = fp16x3_dw_bound(r["A"][l], r["G"][l])
+            lim = 1e-5 * np.abs(w) + F16X3_COL_TOL * cm + 2.0 * bound
+            assert (err <= lim).all(), (l, float((err / np.maximum(lim, 1e-300)).max()))
+            live = cm[0] > 0
+            if live.any():
+                worst_col = max(worst_col, float((err.max(axis=0)[live] / cm[0][live]).max()))
+            worst_bound = max(worst_bound, float((err / np.maximum(lim, 1e-300)).max()))
+        print(f"{name} fp16x3 dW: worst per-column error / column max {worst_col:.3g}, "
+              f"worst error / (column bar + split bound) {worst_bound:.3g}")
     else:
         close_grouped("dW", got["dW"], g["dW"])
     close_grouped("dB", got["dB"], g["dB"])

@@ -297,7 +297,13 @@ __device__ __forceinline__ bf8 lds_frag(const unsigned char* base) {
     return *(const bf8*)(base + OFF);
 }
 
-constexpr int kDist = 2;   // weight tiles read ahead of the one the MFMAs consume
+#ifndef LNERF_K16_KDIST
+#define LNERF_K16_KDIST 2
+#endif
+constexpr int kDist = LNERF_K16_KDIST;   // weight tiles read ahead of the one the MFMAs consume
+#ifndef LNERF_K16_SCHED
+#define LNERF_K16_SCHED 1
+#endif
 
 // timing experiments only (wrong results): read one plane per tile / skip the operand split
 #ifndef LNERF_K16_HALFLDS
@@ -351,6 +357,10 @@ __device__ __forceinline__ void tile_step(const unsigned char* base, bf8 (&w)[kD
     if constexpr (O + kDist < NTO) read_tile<PL, O + kDist>(base, w[(O + kDist) % (kDist + 1)]);
     if constexpr (FD) dma_pieces_at<NTO, O, NW, true>(job, std::make_integer_sequence<int, kPiecesMax>{});
     else if (job.n) dma_pieces_at<NTO, O, NW, false>(job, std::make_integer_sequence<int, kPiecesMax>{});
+    // keep tile O + kDist's reads ahead of tile O's MFMAs: the machine scheduler otherwise sinks
+    // each read next to its first consumer (one MFMA of slack, an LDS round trip exposed per tile);
+    // the compiler still places every wait itself
+    if constexpr (LNERF_K16_SCHED) __builtin_amdgcn_sched_barrier(0);
     bf8(&c)[3] = w[O % (kDist + 1)];
     fx4 acc = out[O];
     if constexpr (PL == 2) {
@@ -469,7 +479,8 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
     bf8 w[kDist + 1][3];
     read_tile<PL, 0>(base, w[0]);
     if constexpr (NTO > 1) read_tile<PL, 1>(base, w[1]);
-    static_assert(kDist == 2, "the prologue reads kDist tiles");
+    if constexpr (NTO > 2 && kDist > 2) read_tile<PL, 2>(base, w[2]);
+    static_assert(kDist == 2 || kDist == 3, "the prologue reads kDist tiles");
     if (st && !spread) store_slab_step(slab + s * 1024, in[2 * s], in[2 * s + 1]);
     // first half of the output tiles, [late waves: barrier], the next k-step's operand split (off
     // the next prologue's critical path), second half, [spread: the slab stores, younger than

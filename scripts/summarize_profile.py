@@ -59,7 +59,7 @@ def main():
     write = per_kernel(os.path.join(src, "write", "run_counter_collection.csv"))
     kernels = {}
     for k in sorted(set(fetch) | set(write)):
-        if not k.startswith(("k16", "dw", "grad_reduce", "loss_reduce", "pack", "wmax16", "k1_reduce", "adam")):
+        if not k.startswith(("k16", "kr_", "dw", "grad_reduce", "loss_reduce", "pack", "wmax16", "k1_reduce", "adam")):
             continue
         f = fetch.get(k, 0.0) * 1024
         w = write.get(k, 0.0) * 1024

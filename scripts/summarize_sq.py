@@ -28,7 +28,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-KEEP = ("k16_fwd_bwd_kernel", "dw16_kernel", "grad_reduce_kernel", "k1_reduce_kernel", "pack16_kernel",
+KEEP = ("k16_fwd_bwd_kernel", "kr_fwd_kernel", "dw16_kernel", "grad_reduce_kernel", "k1_reduce_kernel", "pack16_kernel",
         "adam_kernel", "loss_reduce_kernel")
 
 

@@ -20,6 +20,9 @@
 #include <thread>
 #include <vector>
 
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include "lnerf_internal.h"
 
 using namespace lnerf;
@@ -97,12 +100,13 @@ struct CompatCtx {
 // One CompatCtx per calling thread, freed when that thread exits (its stream and staging go with
 // it). The main thread's context is left to process teardown: at exit() its thread_local
 // destructor may run after the HIP runtime has begun shutting down, where hipStreamDestroy is
-// not safe.
-const std::thread::id g_main_thread = std::this_thread::get_id();
+// not safe. The main thread is the one whose kernel thread id is the process id (whichever
+// thread happened to load the library).
+bool on_main_thread() { return (pid_t)syscall(SYS_gettid) == getpid(); }
 struct CompatHolder {
     CompatCtx* ctx = nullptr;
     ~CompatHolder() {
-        if (ctx && std::this_thread::get_id() != g_main_thread) delete ctx;
+        if (ctx && !on_main_thread()) delete ctx;
     }
 };
 thread_local CompatHolder tl_compat;

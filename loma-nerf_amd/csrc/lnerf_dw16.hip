@@ -47,7 +47,13 @@ constexpr int kRows = 512;                  // A rows [0, 256) and G rows [256, 
 // one plane of a half-block: [16 samples][512 features] 16-bit, each sample's row padded by 64 B
 // so that the 4 sample rows one ds_read_b64_tr_b16 lane group reads start 16 banks apart
 // (conflict-free reads; the ds_write_b64 image writes see a 2-way conflict)
-constexpr int kImgRow = kRows * 2 + 64;
+#ifndef LNERF_DW16_SWZ
+#define LNERF_DW16_SWZ 1
+#endif
+// SWZ: rows of exactly 1 KiB with the 8-B feature quads XOR-swizzled per row (conflict-free writes
+// and reads); else rows padded by 64 B (conflict-free reads, 2-way conflicted writes)
+constexpr int kImgRow = kRows * 2 + (LNERF_DW16_SWZ ? 0 : 64);
+__host__ __device__ constexpr int swz(int row) { return LNERF_DW16_SWZ ? (0x18140C00 >> (8 * (row & 3))) & 0xFF : 0; }
 constexpr int kPlaneBytes = 16 * kImgRow;
 // PL planes per operand: 3 = bf16x6, 2 = fp16x3, 1 = bf16 (all split x 2^e, per-sample shifts)
 template <int PL>
@@ -175,7 +181,7 @@ __device__ __forceinline__ void split4(const fx4& x, bf4& h, bf4& m, bf4& lo) {
 template <int PL>
 __device__ __forceinline__ void write_planes_row(const fx4& v, int i, unsigned char* img, float sa, float sg,
                                                  const RowMap& m) {
-    unsigned char* p = img + m.isamp * kImgRow + image_row(i, m) * 2;
+    unsigned char* p = img + m.isamp * kImgRow + 8 * ((image_row(i, m) >> 2) ^ swz(m.isamp));
     const float sc = i < 2 ? sa : sg;
     if constexpr (PL == 2) {
         typedef unsigned u2 __attribute__((ext_vector_type(2)));
@@ -234,9 +240,11 @@ __device__ __forceinline__ bf8 read_frag(unsigned char* addr) {
 // This lane's byte offset inside a plane for a fragment starting at feature 0: lane 4 q + p of
 // each 16-lane group supplies sample row 8 (l >> 5) + q, features 16 ((l >> 4) & 1) + 4 p ..+3
 // (ds_read_b64_tr_b16 hands lane i of the group feature i of the 4 rows).
-__device__ __forceinline__ int frag_lane_off() {
+__device__ __forceinline__ int frag_off(int f0) {
     const int l = threadIdx.x & 63;
-    return (8 * (l >> 5) + ((l >> 2) & 3)) * kImgRow + (16 * ((l >> 4) & 1) + 4 * (l & 3)) * 2;
+    const int row = 8 * (l >> 5) + ((l >> 2) & 3);
+    const int quad = (f0 >> 2) + 4 * ((l >> 4) & 1) + (l & 3);
+    return row * kImgRow + 8 * (quad ^ swz(row));
 }
 
 // The wave's TI x TJ tile block (TI 32-row tiles of A, TJ of G) on one half-block image, with
@@ -245,16 +253,19 @@ __device__ __forceinline__ int frag_lane_off() {
 // split's last half-block the zeroed loads land in the idle image buffer).
 template <int PL, int TI, int TJ, bool ACTIVE, bool FULL>
 __device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int g0, fx16 (&acc)[TI][TJ],
-                                          const Loads& nl, unsigned char* nxt, const RowMap& m, int E) {
+                                          const Loads& nl, unsigned char* nxt, const RowMap& m, int E,
+                                          bool live = true) {
     float sa, sg;
     sample_scales(nl.e, E, sa, sg);
-    unsigned char* fl = (unsigned char*)img + frag_lane_off();
+    sa = live ? sa : 0.0f;
+    sg = live ? sg : 0.0f;
+    const unsigned char* fl = img;
     bf8 ap[TI][PL];
     if constexpr (ACTIVE) {
 #pragma unroll
         for (int i = 0; i < TI; ++i)
 #pragma unroll
-            for (int p = 0; p < PL; ++p) ap[i][p] = read_frag(fl + p * kPlaneBytes + (a0 + 32 * i) * 2);
+            for (int p = 0; p < PL; ++p) ap[i][p] = read_frag((unsigned char*)fl + p * kPlaneBytes + frag_off(a0 + 32 * i));
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -266,7 +277,7 @@ __device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int 
                 const int j = k < TJ ? k : 0;
                 bf8 gp[PL];
 #pragma unroll
-                for (int p = 0; p < PL; ++p) gp[p] = read_frag(fl + p * kPlaneBytes + (256 + g0 + 32 * j) * 2);
+                for (int p = 0; p < PL; ++p) gp[p] = read_frag((unsigned char*)fl + p * kPlaneBytes + frag_off(256 + g0 + 32 * j));
 #pragma unroll
                 for (int i = 0; i < TI; ++i) {
                     fx16 c = acc[i][j];
@@ -309,7 +320,7 @@ __device__ __forceinline__ void hb_step3(const float* A, const float* G, const u
         dbs[1] += nx.v[3];
     }
     const int cur = (hb - hb0) & 1;
-    block_mma<PL, TI, TJ, ACTIVE, FULL>(lds + cur * kIB, a0, g0, acc, nx, lds + (cur ^ 1) * kIB, m, E);
+    block_mma<PL, TI, TJ, ACTIVE, FULL>(lds + cur * kIB, a0, g0, acc, nx, lds + (cur ^ 1) * kIB, m, E, hb + 1 < hb1);
     __syncthreads();
 }
 
@@ -318,14 +329,13 @@ __device__ __forceinline__ void hb_loop3(const float* A, const float* G, const u
                                          const RowMap& m, int hb0, int hb1, int a0, int g0, fx16 (&acc)[TI][TJ],
                                          Loads& L0, Loads& L1, Loads& L2, fx4 (&dbs)[2], unsigned char* lds,
                                          int E) {
-    int hb = hb0;
-    for (; hb + 3 <= hb1; hb += 3) {
+    // whole triples only (one loop body; remainder copies make the compiler spill the
+    // accumulators): the steps past hb1 split zero-scaled (zero) planes and add nothing
+    for (int hb = hb0; hb < hb1; hb += 3) {
         hb_step3<PL, TI, TJ, ACTIVE, FULL, 0>(A, G, se, kt, nt, m, hb, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
         hb_step3<PL, TI, TJ, ACTIVE, FULL, 1>(A, G, se, kt, nt, m, hb + 1, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
         hb_step3<PL, TI, TJ, ACTIVE, FULL, 2>(A, G, se, kt, nt, m, hb + 2, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
     }
-    if (hb < hb1) hb_step3<PL, TI, TJ, ACTIVE, FULL, 0>(A, G, se, kt, nt, m, hb, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
-    if (hb + 1 < hb1) hb_step3<PL, TI, TJ, ACTIVE, FULL, 1>(A, G, se, kt, nt, m, hb + 1, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
 }
 
 // Two half-blocks in flight (LNERF_DW16_DEPTH = 2): the same rotation over two register sets --
@@ -345,7 +355,7 @@ __device__ __forceinline__ void hb_step2(const float* A, const float* G, const u
         dbs[1] += nx.v[3];
     }
     const int cur = (hb - hb0) & 1;
-    block_mma<PL, TI, TJ, ACTIVE, FULL>(lds + cur * kIB, a0, g0, acc, nx, lds + (cur ^ 1) * kIB, m, E);
+    block_mma<PL, TI, TJ, ACTIVE, FULL>(lds + cur * kIB, a0, g0, acc, nx, lds + (cur ^ 1) * kIB, m, E, hb + 1 < hb1);
     __syncthreads();
 }
 
@@ -353,12 +363,10 @@ template <int PL, int TI, int TJ, bool ACTIVE, bool FULL>
 __device__ __forceinline__ void hb_loop2(const float* A, const float* G, const unsigned short* se, int kt, int nt,
                                          const RowMap& m, int hb0, int hb1, int a0, int g0, fx16 (&acc)[TI][TJ],
                                          Loads& L0, Loads& L1, fx4 (&dbs)[2], unsigned char* lds, int E) {
-    int hb = hb0;
-    for (; hb + 2 <= hb1; hb += 2) {
+    for (int hb = hb0; hb < hb1; hb += 2) {
         hb_step2<PL, TI, TJ, ACTIVE, FULL, 0>(A, G, se, kt, nt, m, hb, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E);
         hb_step2<PL, TI, TJ, ACTIVE, FULL, 1>(A, G, se, kt, nt, m, hb + 1, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E);
     }
-    if (hb < hb1) hb_step2<PL, TI, TJ, ACTIVE, FULL, 0>(A, G, se, kt, nt, m, hb, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E);
 }
 
 // One split of layer l with TI x TJ tile blocks per wave (the layer's ceil(KT/TI) x ceil(NT/TJ)

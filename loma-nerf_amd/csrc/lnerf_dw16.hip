@@ -34,9 +34,6 @@ typedef _Float16 hf4 __attribute__((ext_vector_type(4)));
 #ifndef LNERF_DW16_NOMMA
 #define LNERF_DW16_NOMMA 0
 #endif
-#ifndef LNERF_DW16_NOLOAD
-#define LNERF_DW16_NOLOAD 0
-#endif
 // half-blocks of slab loads in flight per thread (3: default; 2: 17 fewer registers)
 #ifndef LNERF_DW16_DEPTH
 #define LNERF_DW16_DEPTH 3
@@ -147,19 +144,49 @@ __device__ __forceinline__ void sample_shifts(unsigned e, int E, int& ea, int& e
 // Always four loads from valid addresses and no select on the data (nothing waits for it before
 // its use): rows past the layer's tiles are never split, half-blocks past the split land in the
 // idle image and add nothing to db (the callers' hb < hb1 guards).
+template <bool A24>
 __device__ __forceinline__ void issue_loads(const float* A, const float* G, const unsigned short* se, int kt,
                                             int nt, const RowMap& m, int hb, int hb_end, Loads& L) {
     const bool in = hb < hb_end;
     const int hbc = in ? hb : max(0, hb_end - 1);
     L.e = se[hbc * 16 + m.isamp];
     const int blk = hbc >> 1, half = hbc & 1;
-    const float* pa = A + (size_t)blk * kt * 1024 + half * m.hstride;
     const float* pg = G + (size_t)blk * nt * 1024 + half * m.hstride;
+    if constexpr (A24) {
+        // int24 A slab (k1 store_slab_step24): a tile-block is 3 KiB, its half-blocks 1.5 KiB
+        // [h][n][16 f] x 3 B, so thread u's 4 values are the 12 B at 12 u
+        // (three dword loads the compiler merges into one global_load_dwordx3: a nontemporal load
+        // of a 3-element vector type keeps only its first element)
+        const unsigned char* pa = (const unsigned char*)A + ((size_t)blk * kt * 3072 + half * 1536 + 12 * (threadIdx.x & 127));
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const fx4* p = (const fx4*)((i < 2 ? pa : pg) + m.tile[i] * 1024 + m.lane);
-        L.v[i] = LNERF_DW16_NOLOAD ? fx4{1.0f, 2.0f, 3.0f, (float)i} : __builtin_nontemporal_load(p);
+        for (int i = 0; i < 2; ++i) {
+            const unsigned* q = (const unsigned*)(pa + m.tile[i] * 3072);
+            L.v[i] = fx4{__builtin_bit_cast(float, __builtin_nontemporal_load(q)),
+                         __builtin_bit_cast(float, __builtin_nontemporal_load(q + 1)),
+                         __builtin_bit_cast(float, __builtin_nontemporal_load(q + 2)), 0.0f};
+        }
+    } else {
+        const float* pa = A + (size_t)blk * kt * 1024 + half * m.hstride;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) L.v[i] = __builtin_nontemporal_load((const fx4*)(pa + m.tile[i] * 1024 + m.lane));
     }
+#pragma unroll
+    for (int i = 2; i < 4; ++i) L.v[i] = __builtin_nontemporal_load((const fx4*)(pg + m.tile[i] * 1024 + m.lane));
+}
+
+// The 4 values of an int24 A round (k1 store_slab_step24): 3 dwords holding the low 24 bits of
+// y_i = 1.5 2^23 + q_i (q_i = rint(x_i 2^(xa + 8)), |q_i| < 2^22, so y_i lies in [2^23, 2^24)
+// where its mantissa field is y_i - 2^23): q_i = float(0x4B000000 | bits) - 1.5 2^23, exact.
+__device__ __forceinline__ fx4 decode_a24(const fx4& raw) {
+    const unsigned d0 = __builtin_bit_cast(unsigned, raw[0]), d1 = __builtin_bit_cast(unsigned, raw[1]),
+                   d2 = __builtin_bit_cast(unsigned, raw[2]);
+    const unsigned m0 = d0 & 0xFFFFFFu;
+    const unsigned m1 = __builtin_amdgcn_alignbit(d1, d0, 24) & 0xFFFFFFu;
+    const unsigned m2 = __builtin_amdgcn_alignbit(d2, d1, 16) & 0xFFFFFFu;
+    const unsigned m3 = d2 >> 8;
+    constexpr float kMagic = 12582912.0f;   // 1.5 2^23
+    return fx4{__builtin_bit_cast(float, 0x4B000000u | m0) - kMagic, __builtin_bit_cast(float, 0x4B000000u | m1) - kMagic,
+               __builtin_bit_cast(float, 0x4B000000u | m2) - kMagic, __builtin_bit_cast(float, 0x4B000000u | m3) - kMagic};
 }
 
 // x = hi + mid + lo, round-to-nearest bf16 of each remainder (every remainder is exact in f32).
@@ -190,6 +217,9 @@ __device__ __forceinline__ void write_planes_row(const fx4& v, int i, unsigned c
         split_h2(v[2], v[3], sc, h1, l1);
         *(u2*)(p) = u2{h0, h1};
         *(u2*)(p + kPlaneBytes) = u2{l0, l1};
+    } else if constexpr (PL == 1) {
+        const fx4 x = v * sc;
+        *(bf4*)(p) = bf4{(__bf16)x[0], (__bf16)x[1], (__bf16)x[2], (__bf16)x[3]};
     } else {
         bf4 h, m, lo;
         split4(v * sc, h, m, lo);
@@ -199,20 +229,34 @@ __device__ __forceinline__ void write_planes_row(const fx4& v, int i, unsigned c
     }
 }
 
-// the split scales 2^ea (A rows) and 2^eg (G rows) of a half-block's sample (sample_shifts)
+// the split scales 2^ea (A rows) and 2^eg (G rows) of a half-block's sample (sample_shifts); with
+// int24 A slabs the A values arrive as q = x 2^(xa + 8), so their scale is 2^(ea - xa - 8) (1 for an
+// all-zero row, whose q are 0)
+template <int PL>
 __device__ __forceinline__ void sample_scales(unsigned e, int E, float& sa, float& sg) {
     int ea, eg;
     sample_shifts(e, E, ea, eg);
+    if constexpr (a24_slabs(PL)) {
+        const int xa = (int)(signed char)(e & 0xFFu);
+        ea = xa == -128 ? 0 : ea - xa - 8;
+    }
     sa = __builtin_ldexpf(1.0f, ea);
     sg = __builtin_ldexpf(1.0f, eg);
+}
+
+// round i's values as the split takes them (int24 A rounds decoded)
+template <int PL>
+__device__ __forceinline__ fx4 round_values(const Loads& L, int i) {
+    if constexpr (a24_slabs(PL)) return i < 2 ? decode_a24(L.v[i]) : L.v[i];
+    return L.v[i];
 }
 
 template <int PL>
 __device__ __forceinline__ void write_planes(const Loads& L, unsigned char* img, int E, const RowMap& m) {
     float sa, sg;
-    sample_scales(L.e, E, sa, sg);
+    sample_scales<PL>(L.e, E, sa, sg);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) write_planes_row<PL>(L.v[i], i, img, sa, sg, m);
+    for (int i = 0; i < 4; ++i) write_planes_row<PL>(round_values<PL>(L, i), i, img, sa, sg, m);
 }
 
 __device__ __forceinline__ fx16 mfma32(const bf8& a, const bf8& b, fx16 c) {
@@ -256,7 +300,7 @@ __device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int 
                                           const Loads& nl, unsigned char* nxt, const RowMap& m, int E,
                                           bool live = true) {
     float sa, sg;
-    sample_scales(nl.e, E, sa, sg);
+    sample_scales<PL>(nl.e, E, sa, sg);
     sa = live ? sa : 0.0f;
     sg = live ? sg : 0.0f;
     const unsigned char* fl = img;
@@ -271,7 +315,7 @@ __device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int 
     for (int k = 0; k < 4; ++k) {
         // rows past the layer's tiles are never read: skip their split (wave-uniform: a wave's
         // values of a round lie in one 32-feature tile); FULL layers need no branch
-        if (FULL || m.ok[k]) write_planes_row<PL>(nl.v[k], k, nxt, sa, sg, m);
+        if (FULL || m.ok[k]) write_planes_row<PL>(round_values<PL>(nl, k), k, nxt, sa, sg, m);
         if constexpr (ACTIVE) {
             if (k < TJ) {
                 const int j = k < TJ ? k : 0;
@@ -314,7 +358,7 @@ __device__ __forceinline__ void hb_step3(const float* A, const float* G, const u
     constexpr int kIB = image_bytes<PL>();
     Loads& fr = I == 0 ? L0 : I == 1 ? L1 : L2;
     const Loads& nx = I == 0 ? L1 : I == 1 ? L2 : L0;
-    issue_loads(A, G, se, kt, nt, m, hb + 3, hb1, fr);
+    issue_loads<a24_slabs(PL)>(A, G, se, kt, nt, m, hb + 3, hb1, fr);
     if (hb + 1 < hb1) {
         dbs[0] += nx.v[2];
         dbs[1] += nx.v[3];
@@ -349,7 +393,7 @@ __device__ __forceinline__ void hb_step2(const float* A, const float* G, const u
     constexpr int kIB = image_bytes<PL>();
     Loads& fr = I == 0 ? L0 : L1;
     const Loads& nx = I == 0 ? L1 : L0;
-    issue_loads(A, G, se, kt, nt, m, hb + 2, hb1, fr);
+    issue_loads<a24_slabs(PL)>(A, G, se, kt, nt, m, hb + 2, hb1, fr);
     if (hb + 1 < hb1) {
         dbs[0] += nx.v[2];
         dbs[1] += nx.v[3];
@@ -401,8 +445,8 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
     const bool full = KT == 8 && NT == 8;
 #if LNERF_DW16_DEPTH == 2
     Loads L0, L1;
-    issue_loads(A, G, se, KT, NT, m, hb0, hb1, L0);
-    issue_loads(A, G, se, KT, NT, m, hb0 + 1, hb1, L1);
+    issue_loads<a24_slabs(PL)>(A, G, se, KT, NT, m, hb0, hb1, L0);
+    issue_loads<a24_slabs(PL)>(A, G, se, KT, NT, m, hb0 + 1, hb1, L1);
     if (hb0 < hb1) {
         dbs[0] += L0.v[2];
         dbs[1] += L0.v[3];
@@ -415,9 +459,9 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
     else hb_loop2<PL, TI, TJ, false, false>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E);
 #else
     Loads L0, L1, L2;
-    issue_loads(A, G, se, KT, NT, m, hb0, hb1, L0);
-    issue_loads(A, G, se, KT, NT, m, hb0 + 1, hb1, L1);
-    issue_loads(A, G, se, KT, NT, m, hb0 + 2, hb1, L2);
+    issue_loads<a24_slabs(PL)>(A, G, se, KT, NT, m, hb0, hb1, L0);
+    issue_loads<a24_slabs(PL)>(A, G, se, KT, NT, m, hb0 + 1, hb1, L1);
+    issue_loads<a24_slabs(PL)>(A, G, se, KT, NT, m, hb0 + 2, hb1, L2);
     if (hb0 < hb1) {
         dbs[0] += L0.v[2];
         dbs[1] += L0.v[3];

@@ -134,7 +134,10 @@ struct Layout {
 };
 
 // train = false (render): no slabs, masks or dW partials (the forward-only kernel writes none).
-void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S, bool train, int dw_grid, int tile) {
+// a_tile: float slots per 32 x 32 tile-block of an activation slab (a_tile_floats: 768 for int24 A
+// slabs, 1024 for fp32; the workspace is sized with 1024)
+void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S, bool train, int dw_grid, int tile,
+                 int a_tile = 1024) {
     const int L = m.num_layers;
     int kt[kMaxLayers], nt[kMaxLayers];
     for (int l = 0; l < L; ++l) {
@@ -163,8 +166,8 @@ void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S, bool train, int
     y.mask_total = train ? (size_t)y.num_wg * (L > 1 ? L - 1 : 0) * (tile / 16) * 64 : 0;
     y.blocks = y.num_wg * (tile / 32);
     off = 0;
-    y.x_off = off; off += (size_t)y.blocks * kt[0] * 1024;
-    for (int l = 0; l < L - 1; ++l) { y.act_off[l] = off; off += (size_t)y.blocks * nt[l] * 1024; }
+    y.x_off = off; off += (size_t)y.blocks * kt[0] * a_tile;
+    for (int l = 0; l < L - 1; ++l) { y.act_off[l] = off; off += (size_t)y.blocks * nt[l] * a_tile; }
     y.act_total = train ? off : 0;
     off = 0;
     for (int l = 0; l < L; ++l) { y.grad_off[l] = off; off += (size_t)y.blocks * nt[l] * 1024; }
@@ -240,12 +243,13 @@ size_t fused_workspace_bytes(const lnerf_mlp& m, int rays, int S, bool train, in
 
 static void fused_plan_tile(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws_base, int flags,
                             bool train, int dw_grid, int tile) {
+    const int x6 = (flags & LNERF_MFMA_BF16) ? 1 : (flags & LNERF_MFMA_BF16X6) ? 3 : 2;   // fp16x3 default
     Layout y;
-    make_layout(y, m, b.rays, b.samples, train, dw_grid, tile);
+    make_layout(y, m, b.rays, b.samples, train, dw_grid, tile, a_tile_floats(x6));
     p = FusedPlan{};
     p.tile = tile;
     p.L = m.num_layers;
-    p.x6 = (flags & LNERF_MFMA_BF16) ? 1 : (flags & LNERF_MFMA_BF16X6) ? 3 : 2;   // fp16x3 default
+    p.x6 = x6;
     for (int l = 0; l < p.L; ++l) {
         p.k[l] = m.k[l];
         p.n[l] = m.n[l];

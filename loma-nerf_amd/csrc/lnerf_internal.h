@@ -44,6 +44,19 @@ __device__ __forceinline__ void split_h2(float x0, float x1, float sc, unsigned&
     lo = __builtin_bit_cast(unsigned, (h2){l0, l1});
 }
 
+// ---- int24 activation slabs (fp16x3 training) --------------------------------------------------
+// k1 stores each A_l value (X for l = 0) that k2 reads as q = rint(x 2^(xa + 8)), xa = the
+// sample's row shift (fp16x3_shift of its max|x|, so |q| < 2^22), as the low 24 bits of the float
+// 1.5 2^23 + q (whose mantissa field is 2^22 + q); 4 values in 12 B. 2^-22 of the row's max|x|,
+// the precision fp16x3 keeps of it anyway; 25 % fewer bytes through HBM for the A half of the
+// slabs. G_l slabs stay fp32 (their rows span more range: tests/test_gpu_edge.py). A tile-block
+// (32 samples x 32 features) is then 3 KiB = 768 float slots instead of 1024.
+#ifndef LNERF_A24
+#define LNERF_A24 0
+#endif
+__host__ __device__ constexpr bool a24_slabs(int PL) { return PL == 2 && LNERF_A24 != 0; }
+__host__ __device__ constexpr int a_tile_floats(int PL) { return a24_slabs(PL) ? 768 : 1024; }
+
 // ---- ray sampling (train_nerf.py:289-306), float64 as numpy computes it -----------------------
 // t_j = np.linspace(near, far, S)[j]: j * ((far - near) / (S - 1)) + near, the last one = far.
 __host__ __device__ inline double ray_depth(int j, int S, float near_t, float far_t) {

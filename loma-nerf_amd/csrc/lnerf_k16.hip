@@ -291,6 +291,26 @@ __device__ __forceinline__ void store_slab_step(float* __restrict__ dst, const f
     __builtin_nontemporal_store(t1, (fx4*)(dst + 256 + n * 16 + 4 * g));
 }
 
+// The same k-step store for an int24 activation slab (lnerf_internal.h a24_slabs): the 8 values
+// as y = x 2^(ex + 8) + 1.5 2^23 (round-to-nearest integer q in the mantissa field, |q| < 2^22;
+// ex = the sample's row shift), their low 24 bits packed 4 to 12 B by v_perm_b32, two
+// global_store_dwordx3 into the 1.5-KiB half-block run [feature half 2][16 samples][16 f] x 3 B.
+__device__ __forceinline__ void store_slab_step24(unsigned char* __restrict__ dst, const fx4& t0, const fx4& t1,
+                                                  int ex) {
+    typedef unsigned u3 __attribute__((ext_vector_type(3)));
+    const int lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
+    constexpr float kMagic = 12582912.0f;   // 1.5 2^23
+    auto pack = [&](const fx4& t) {
+        unsigned y[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) y[i] = __builtin_bit_cast(unsigned, __builtin_ldexpf(t[i], ex + 8) + kMagic);
+        return u3{__builtin_amdgcn_perm(y[1], y[0], 0x04020100u), __builtin_amdgcn_perm(y[2], y[1], 0x05040201u),
+                  __builtin_amdgcn_perm(y[3], y[2], 0x06050402u)};
+    };
+    __builtin_nontemporal_store(pack(t0), (u3*)(dst + n * 48 + 12 * g));
+    __builtin_nontemporal_store(pack(t1), (u3*)(dst + 768 + n * 48 + 12 * g));
+}
+
 // A weight fragment: one ds_read_b128 per lane (the compiler counts it and places its wait).
 template <int OFF>
 __device__ __forceinline__ bf8 lds_frag(const unsigned char* base) {
@@ -343,24 +363,9 @@ __device__ __forceinline__ void dma_piece(const DmaJob& j, int p) {
 }
 // the pieces that land on output tile O: p with p * NTO / kPiecesMax == O (all on tile 0 when NTO == 1);
 // FULL: the chunk is known to be whole (every wave issues kPiecesMax pieces, no per-piece test)
-// DMASTAG: the two waves of a SIMD (w and w + NW/2) issue their pieces in different halves of the
-// output tiles, so that while one pays a piece's issue cost (~60-185 cycles, MI355X_MICROARCH.md)
-// its partner issues MFMAs (in lockstep both stall at once)
-#ifndef LNERF_K16_DMASTAG
-#define LNERF_K16_DMASTAG 0
-#endif
 template <int NTO, int O, int NW, bool FULL, int... P>
 __device__ __forceinline__ void dma_pieces_at(const DmaJob& j, std::integer_sequence<int, P...>) {
-    if constexpr (LNERF_K16_DMASTAG && NTO >= 2) {
-        constexpr int H = NTO / 2;
-        const bool late = wave_id() >= NW / 2;
-        if (O < H ? !late : late)
-            ((((P * H) / kPiecesMax == (O < H ? O : O - H)) ? ((FULL || P < j.n) ? dma_piece<NW>(j, P) : void())
-                                                           : void()),
-             ...);
-    } else {
-        (((P * NTO) / kPiecesMax == O ? ((FULL || P < j.n) ? dma_piece<NW>(j, P) : void()) : void()), ...);
-    }
+    (((P * NTO) / kPiecesMax == O ? ((FULL || P < j.n) ? dma_piece<NW>(j, P) : void()) : void()), ...);
 }
 
 // Output tile O of one k-step: issue the reads of tile O + kDist, the MFMAs of tile O (small
@@ -450,7 +455,7 @@ __device__ __forceinline__ void make_b(const fx4 (&in)[kMaxT], int s, int ex, bf
 // (the A_{l-1} or G_l slab of this wave's half-block).
 // FD: this k-step issues the DMA of a chunk known to be whole (the next chunk of the same full
 // pass): kPiecesMax pieces per wave with no per-piece test and no byte arithmetic.
-template <int NTO, int PL, int NW, bool FD = false>
+template <int NTO, int PL, int NW, bool FD = false, bool A24 = false>
 __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk, bool last, int& ci,
                                          unsigned char* ring, float* bias_ring, const fx4 (&in)[kMaxT],
                                          fx4 (&out)[kMaxT], float* __restrict__ slab, int ex, bf8& bh,
@@ -496,7 +501,11 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
     if constexpr (NTO > 1) read_tile<PL, 1>(base, w[1]);
     if constexpr (NTO > 2 && kDist > 2) read_tile<PL, 2>(base, w[2]);
     static_assert(kDist == 2 || kDist == 3, "the prologue reads kDist tiles");
-    if (st && !spread) store_slab_step(slab + s * 1024, in[2 * s], in[2 * s + 1]);
+    auto store = [&]() {
+        if constexpr (A24) store_slab_step24((unsigned char*)slab + s * 3072, in[2 * s], in[2 * s + 1], ex);
+        else store_slab_step(slab + s * 1024, in[2 * s], in[2 * s + 1]);
+    };
+    if (st && !spread) store();
     // first half of the output tiles, [late waves: barrier], the next k-step's operand split (off
     // the next prologue's critical path), second half, [spread: the slab stores, younger than
     // every piece], [early: barrier]
@@ -508,7 +517,7 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
     tile_steps<NTO, PL, NW, FD, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, bh, bm, bl, out, job);
     if (st && spread) {
         asm volatile("" ::: "memory");
-        store_slab_step(slab + s * 1024, in[2 * s], in[2 * s + 1]);
+        store();
     }
     if (!late && last) dma_barrier(pending);
     if (last) ++ci;
@@ -520,7 +529,7 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
 // One k-step S of a pass. FULL: the pass has all 8 k-steps (a 256-wide input), so the step
 // bounds are compile-time and, where the chunk after this one belongs to the same pass and is
 // whole (KC NTO PL KiB = kPiecesMax pieces per wave), its DMA is issued without per-piece tests.
-template <int NTO, int PL, int NW, bool FULL, int S>
+template <int NTO, int PL, int NW, bool FULL, bool A24, int S>
 __device__ __forceinline__ void k16_pass_step(const K16Args& a, int ks, int& ci, unsigned char* ring,
                                               float* bias_ring, const fx4 (&in)[kMaxT], fx4 (&out)[kMaxT],
                                               float* __restrict__ slab, int ex, bf8& bh, bf8& bm, bf8& bl,
@@ -531,41 +540,42 @@ __device__ __forceinline__ void k16_pass_step(const K16Args& a, int ks, int& ci,
         const bool last = kk == KC - 1 || (FULL ? S == 7 : S + 1 == ks);
         constexpr bool fd = LNERF_K16_FULLDMA && FULL && kk == 0 && S / KC + 1 < 8 / KC &&
                             KC * NTO * PL == kPiecesMax * NW && LNERF_K16_SPREAD && !Ring<PL, NW>::stagger;
-        k16_step<NTO, PL, NW, fd>(a, FULL ? 8 : ks, S, kk, last, ci, ring, bias_ring, in, out, slab, ex, bh, bm,
-                                  bl, pending);
+        k16_step<NTO, PL, NW, fd, A24>(a, FULL ? 8 : ks, S, kk, last, ci, ring, bias_ring, in, out, slab, ex, bh,
+                                       bm, bl, pending);
     }
 }
-template <int NTO, int PL, int NW, bool FULL, int... S>
+template <int NTO, int PL, int NW, bool FULL, bool A24, int... S>
 __device__ __forceinline__ void k16_pass_steps(std::integer_sequence<int, S...>, const K16Args& a, int ks, int& ci,
                                                unsigned char* ring, float* bias_ring, const fx4 (&in)[kMaxT],
                                                fx4 (&out)[kMaxT], float* __restrict__ slab, int ex, bf8& bh,
                                                bf8& bm, bf8& bl, int& pending) {
-    (k16_pass_step<NTO, PL, NW, FULL, S>(a, ks, ci, ring, bias_ring, in, out, slab, ex, bh, bm, bl, pending), ...);
+    (k16_pass_step<NTO, PL, NW, FULL, A24, S>(a, ks, ci, ring, bias_ring, in, out, slab, ex, bh, bm, bl, pending), ...);
 }
 
 // One pass (a layer's forward or backward MMA) over its ks k-steps, Ring::KC k-steps per chunk.
-template <int NTO, int PL, int NW, bool FULL = false>
+// A24: the pass's input slab (a forward pass's A_{l-1}) is int24 (store_slab_step24).
+template <int NTO, int PL, int NW, bool FULL = false, bool A24 = false>
 __device__ __forceinline__ void k16_pass(const K16Args& a, int ks, int& ci, unsigned char* ring,
                                          float* bias_ring, const fx4 (&in)[kMaxT], fx4 (&out)[kMaxT],
                                          float* __restrict__ slab, int ex = 0) {
     bf8 bh = {}, bm = {}, bl = {};
     make_b<PL>(in, 0, ex, bh, bm, bl);
     int pending = 0;
-    k16_pass_steps<NTO, PL, NW, FULL>(std::make_integer_sequence<int, 8>{}, a, ks, ci, ring, bias_ring, in, out, slab,
-                                      ex, bh, bm, bl, pending);
+    k16_pass_steps<NTO, PL, NW, FULL, A24>(std::make_integer_sequence<int, 8>{}, a, ks, ci, ring, bias_ring, in, out,
+                                           slab, ex, bh, bm, bl, pending);
 }
 // a hidden layer's pass: the FULL instantiation for 256-wide inputs (every hidden layer of cfg3)
-template <int HT, int PL, int NW>
+template <int HT, int PL, int NW, bool A24 = false>
 __device__ __forceinline__ void k16_hidden_pass(const K16Args& a, int ks, int& ci, unsigned char* ring,
                                                 float* bias_ring, const fx4 (&in)[kMaxT], fx4 (&out)[kMaxT],
                                                 float* __restrict__ slab, int ex) {
     if constexpr (LNERF_K16_FULLDMA && HT == 16) {
         if (ks == 8) {
-            k16_pass<HT, PL, NW, true>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
+            k16_pass<HT, PL, NW, true, A24>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
             return;
         }
     }
-    k16_pass<HT, PL, NW, false>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
+    k16_pass<HT, PL, NW, false, A24>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
 }
 
 template <int PL, int NW>
@@ -769,10 +779,11 @@ k16_fwd_bwd_kernel(K16Args a) {
 
     // ---- forward ----
     for (int l = 0; l < a.L; ++l) {
+        constexpr int AT = a_tile_floats(PL);   // float slots per activation tile-block (int24: 768)
         float* slab = !st ? nullptr
-                          : (l == 0 ? a.act + a.x_off + blk * (size_t)(a.kt[0] * 1024)
-                                    : a.act + a.act_off[l - 1] + blk * (size_t)(a.kt[l] * 1024)) +
-                                half * 512;
+                          : (l == 0 ? a.act + a.x_off + blk * (size_t)(a.kt[0] * AT)
+                                    : a.act + a.act_off[l - 1] + blk * (size_t)(a.kt[l] * AT)) +
+                                half * (AT / 2);
         zero_tiles(out);
         const float* bl = bias_ring + (l % 3) * 256 + g * 4;
         const float xm = (PL >= 2 || st) ? sample_max(act) : 0.0f;
@@ -781,7 +792,7 @@ k16_fwd_bwd_kernel(K16Args a) {
         const int sh = unscale(l, ex);
         if (l < a.L - 1) {
             PROF_T(t_f);
-            k16_hidden_pass<HT, PL, NW>(a, a.ks_f[l], ci, ring, bias_ring, act, out, slab, ex);
+            k16_hidden_pass<HT, PL, NW, a24_slabs(PL)>(a, a.ks_f[l], ci, ring, bias_ring, act, out, slab, ex);
             PROF_ADD(kPfFwd, t_f);
             PROF_T(t_fe);
             // bias after the sum (nerf.py:98,125), ReLU (nerf.py:141-144) and its mask bits
@@ -801,7 +812,7 @@ k16_fwd_bwd_kernel(K16Args a) {
             if (st) mask_w[(size_t)l * NW * 64] = mb;
             PROF_ADD(kPfFwdEpi, t_fe);
         } else {
-            k16_pass<1, PL, NW>(a, a.ks_f[l], ci, ring, bias_ring, act, out, slab, ex);
+            k16_pass<1, PL, NW, false, a24_slabs(PL)>(a, a.ks_f[l], ci, ring, bias_ring, act, out, slab, ex);
             fx4 bv[kMaxT];
             bias_read<1>(std::make_integer_sequence<int, 1>{}, bl, bv);
             // head pre-activations: features 0..3 = registers 0..3 of lane group 0

@@ -35,8 +35,9 @@ def fp16x3_dw_bound(A, G):
     """Per-element a-priori bound of k2's fp16x3 dW error (lnerf_dw16.hip): every operand x is
     scaled by 2^e (k1's row shift fp16x3_shift, balanced per sample by sample_shifts) and split
     as hi + lo in fp16, so |x 2^e - hi - lo| <= 2^-22 |x 2^e| + 2^-25 (half fp16's subnormal
-    quantum); the dropped lo x lo term adds <= 2^-22 |x 2^e| |y 2^f|. Summed over the samples:
-    3 2^-22 sum |A||G| + sum_s |A[s,k]| 2^-25-eg_s [G != 0] + |G[s,n]| 2^-25-ea_s [A != 0]."""
+    quantum); the dropped lo x lo term adds <= 2^-22 |x 2^e| |y 2^f|; the A values come from k1's
+    int24 slabs, rounded to multiples of 2^-(xa + 8). Summed over the samples:
+    3 2^-22 sum |A||G| + sum_s |A[s,k]| 2^-25-eg_s [G != 0] + |G[s,n]| (2^-25-ea_s + 2^-9-xa_s) [A != 0]."""
     def row_shift(x):
         m = np.abs(x).max(axis=1)
         e = np.zeros(len(m), np.int64)
@@ -54,7 +55,10 @@ def fp16x3_dw_bound(A, G):
     eg = np.where(live, xg - ((d + 1) >> 1), np.where(zg, 0, xg))
     qa = np.ldexp(1.0, -25 - ea)[:, None]
     qg = np.ldexp(1.0, -25 - eg)[:, None]
-    return 3 * 2.0 ** -22 * (A.T @ G) + A.T @ (qg * (G > 0)) + (qa * (A > 0)).T @ G
+    # k1's int24 A slabs (lnerf_internal.h a24_slabs): A rounded to a multiple of 2^-(xa + 8), error
+    # <= 2^-(xa + 9) per nonzero element
+    q24 = np.where(za, 0.0, np.ldexp(1.0, -9 - np.where(za, 0, xa)))[:, None]
+    return 3 * 2.0 ** -22 * (A.T @ G) + A.T @ (qg * (G > 0)) + ((qa + q24) * (A > 0)).T @ G
 
 
 def load(name):

@@ -107,3 +107,20 @@ def test_inline_asm_writes_registers_only_in_place():
                     line = src[:m.start()].count("\n") + 1
                     found.append(f"{fn}:{line}: output constraint {c!r}")
     assert not found, "\n".join(found)
+
+
+def test_int24_activation_slabs_move_12_bytes_per_lane(asm):
+    if "#define LNERF_A24 0" in open(os.path.join(CSRC, "lnerf_internal.h")).read():
+        pytest.skip("int24 activation slabs are off in this build (LNERF_A24 0)")
+    """fp16x3 training writes and reads the A slabs as int24 (lnerf_internal.h a24_slabs): k1
+    stores 12 B per lane (global_store_dwordx3) and k2 loads 12 B per lane (global_load_dwordx3).
+    Guards the round-4 miscompile: a nontemporal load of a 3-element vector type kept only its
+    first element (one global_load_dword), so k2 decoded three quarters of A from garbage."""
+    import isa_check
+    k1 = isa_check.parse_kernels(asm, r"k16_fwd_bwd_kernelILi16ELi2ELi8E")
+    k2 = isa_check.parse_kernels(asm, r"dw16_kernelILi2E")
+    assert k1 and k2
+    for name, insts in k1.items():
+        assert any(i.mn == "global_store_dwordx3" for i in insts), name
+    for name, insts in k2.items():
+        assert any(i.mn == "global_load_dwordx3" for i in insts), name

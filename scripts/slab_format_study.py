@@ -16,7 +16,8 @@ Formats (all take the fp32 value k1 holds):
   hi16+e5m2   k1's own fp16 hi of x 2^e (e = the row's fp16x3 shift) + its fp16 lo rounded to
               e5m2 (the top byte of the fp16 bit pattern): 3 bytes, hi usable by k2 as it is
   hi16+q8     fp16 hi + the lo as a signed 8-bit multiple of ulp(hi)/256: 3 bytes, 19 bits
-  int24       fixed point of x 2^(e+9) per row (|x 2^e| < 2^14): 3 bytes, 2^-24 of the row max
+  int24       fixed point of x 2^(e+8) per row (|x 2^e| < 2^14): 3 bytes, 2^-23 of the row max
+              (the shipped format, lnerf_internal.h a24_slabs)
   A:<format>  only the activation slabs (X, A_l) in the format, the gradient slabs G_l in fp32
 
     python scripts/slab_format_study.py [--rays 256]
@@ -74,10 +75,12 @@ def q_hi16_q8(x32):
 
 
 def q_int24(x32):
+    """The shipped format (lnerf_internal.h a24_slabs): q = rint(x 2^(e + 8)), |q| < 2^22, via the
+    fp32 add of 1.5 2^23 (round to nearest even)."""
     e = row_shift(x32)[:, None]
-    y = np.rint(np.ldexp(x32.astype(np.float64), e + 9))
-    y = np.clip(y, -(2 ** 23 - 1), 2 ** 23 - 1)
-    return np.ldexp(y, -(e + 9)).astype(np.float32)
+    y = np.rint(np.ldexp(x32.astype(np.float64), e + 8))
+    y = np.clip(y, -(2 ** 22 - 1), 2 ** 22 - 1)
+    return np.ldexp(y, -(e + 8)).astype(np.float32)
 
 
 FORMATS = {"fp32": lambda x: x, "top24": q_top24, "hi16+e5m2": q_hi16_e5m2, "hi16+q8": q_hi16_q8,

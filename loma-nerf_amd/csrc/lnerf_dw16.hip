@@ -178,8 +178,12 @@ __device__ __forceinline__ void issue_loads(const float* A, const float* G, cons
 // y_i = 1.5 2^23 + q_i (q_i = rint(x_i 2^(xa + 8)), |q_i| < 2^22, so y_i lies in [2^23, 2^24)
 // where its mantissa field is y_i - 2^23): q_i = float(0x4B000000 | bits) - 1.5 2^23, exact.
 __device__ __forceinline__ fx4 decode_a24(const fx4& raw) {
-    const unsigned d0 = __builtin_bit_cast(unsigned, raw[0]), d1 = __builtin_bit_cast(unsigned, raw[1]),
-                   d2 = __builtin_bit_cast(unsigned, raw[2]);
+    // bit_cast the whole vector: __builtin_bit_cast of an ext_vector element (raw[1]) yields
+    // element 0 in this compiler (ROCm 7.2 clang), which decoded three quarters of A from the
+    // wrong dword
+    typedef unsigned ux4 __attribute__((ext_vector_type(4)));
+    const ux4 d = __builtin_bit_cast(ux4, raw);
+    const unsigned d0 = d[0], d1 = d[1], d2 = d[2];
     const unsigned m0 = d0 & 0xFFFFFFu;
     const unsigned m1 = __builtin_amdgcn_alignbit(d1, d0, 24) & 0xFFFFFFu;
     const unsigned m2 = __builtin_amdgcn_alignbit(d2, d1, 16) & 0xFFFFFFu;

@@ -114,8 +114,9 @@ def test_int24_activation_slabs_move_12_bytes_per_lane(asm):
         pytest.skip("int24 activation slabs are off in this build (LNERF_A24 0)")
     """fp16x3 training writes and reads the A slabs as int24 (lnerf_internal.h a24_slabs): k1
     stores 12 B per lane (global_store_dwordx3) and k2 loads 12 B per lane (global_load_dwordx3).
-    Guards the round-4 miscompile: a nontemporal load of a 3-element vector type kept only its
-    first element (one global_load_dword), so k2 decoded three quarters of A from garbage."""
+    Guards a round-4 miscompile: __builtin_bit_cast of an ext_vector element (raw[1]) yielded
+    element 0, so k2's decode read one dword three times and the compiler narrowed the 12-B load
+    to one global_load_dword (three quarters of A decoded from the wrong bytes)."""
     import isa_check
     k1 = isa_check.parse_kernels(asm, r"k16_fwd_bwd_kernelILi16ELi2ELi8E")
     k2 = isa_check.parse_kernels(asm, r"dw16_kernelILi2E")

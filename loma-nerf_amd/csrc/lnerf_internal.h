@@ -52,7 +52,7 @@ __device__ __forceinline__ void split_h2(float x0, float x1, float sc, unsigned&
 // slabs. G_l slabs stay fp32 (their rows span more range: tests/test_gpu_edge.py). A tile-block
 // (32 samples x 32 features) is then 3 KiB = 768 float slots instead of 1024.
 #ifndef LNERF_A24
-#define LNERF_A24 0
+#define LNERF_A24 1
 #endif
 __host__ __device__ constexpr bool a24_slabs(int PL) { return PL == 2 && LNERF_A24 != 0; }
 __host__ __device__ constexpr int a_tile_floats(int PL) { return a24_slabs(PL) ? 768 : 1024; }

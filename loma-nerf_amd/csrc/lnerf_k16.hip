@@ -76,16 +76,10 @@ constexpr int kCompBytes = 2688 * 4;          // composite_tile's scratch (comp[
 //    chunk apart; the ring then needs 3 slots (the late waves still read the previous chunk
 //    while every wave reads the current one and the next one lands).
 //  * NW = 4 (two workgroups per CU, each within 80 KiB of LDS): KC = 1, two 32 KiB slots.
-// LNERF_K16_STAG2 (A/B knob): fp16x3 on the bf16x6 ring shape too (1-k-step chunks, 3 slots,
-// staggered wave pairs)
-#ifndef LNERF_K16_STAG2
-#define LNERF_K16_STAG2 0
-#endif
 template <int PL, int NW = 8>
 struct Ring {
-    static constexpr bool stag = (PL == 3 || (PL == 2 && LNERF_K16_STAG2)) && NW == 8;
-    static constexpr int KC = (stag || NW == 4) ? 1 : 2;
-    static constexpr bool stagger = stag;
+    static constexpr int KC = (PL == 3 || NW == 4) ? 1 : 2;
+    static constexpr bool stagger = PL == 3 && NW == 8;
     static constexpr int slots = stagger ? 3 : 2;
     static constexpr int slot_bytes = KC * kMaxT * PL * 1024;
     static constexpr int off_comp = slots * slot_bytes;
@@ -1110,7 +1104,7 @@ void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lner
     // the chunk stream: forward 0..L-1, backward L-1..1 (training), backward 0 (d_x); chunks of
     // KC k-steps (Ring: 2 for fp16x3 / bf16, 1 for bf16x6), the pack layout's consecutive k-steps
     {
-        const int KC = (p.x6 == 3 || (p.x6 == 2 && LNERF_K16_STAG2) || p.tile == 64) ? 1 : 2;
+        const int KC = (p.x6 == 3 || p.tile == 64) ? 1 : 2;
         int ci = 0;
         auto add = [&](bool fwd, int l) {
             const int ks = fwd ? a.ks_f[l] : a.ks_b[l], to = fwd ? a.to_f[l] : a.to_b[l];

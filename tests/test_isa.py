@@ -110,8 +110,6 @@ def test_inline_asm_writes_registers_only_in_place():
 
 
 def test_int24_activation_slabs_move_12_bytes_per_lane(asm):
-    if "#define LNERF_A24 0" in open(os.path.join(CSRC, "lnerf_internal.h")).read():
-        pytest.skip("int24 activation slabs are off in this build (LNERF_A24 0)")
     """fp16x3 training writes and reads the A slabs as int24 (lnerf_internal.h a24_slabs): k1
     stores 12 B per lane (global_store_dwordx3) and k2 loads 12 B per lane (global_load_dwordx3).
     Guards a round-4 miscompile: __builtin_bit_cast of an ext_vector element (raw[1]) yielded

@@ -558,9 +558,11 @@ def main():
             out["dw_kernel_tflops"] = dw_flops / (kt["dw"] / 1e3) / 1e12
             out["dw_kernel_frac"] = out["dw_kernel_tflops"] / peak
             # k2 streams the slabs k1 wrote: algorithmic bytes = every slab value read once
-            # (X, A_l for l < L-1, G_l for every l; 32-feature tiles, fp32)
-            slab_b = 4 * 32 * (-(-shapes[0][0] // 32) + sum(-(-n // 32) for _, n in shapes[:-1])
-                               + sum(-(-n // 32) for _, n in shapes))
+            # (X, A_l for l < L-1: 3 B per value as int24 under fp16x3 training, else 4; G_l for
+            # every l: 4 B; 32-feature tiles)
+            a_b = 3 if t.eng.last_path().get("a24") else 4
+            slab_b = 32 * (a_b * (-(-shapes[0][0] // 32) + sum(-(-n // 32) for _, n in shapes[:-1]))
+                           + 4 * sum(-(-n // 32) for _, n in shapes))
             out["dw_kernel_hbm"] = {"kernel": "dw16_kernel<2>", "avg_ms": kt["dw"],
                                     "bytes_per_sample": slab_b, "bytes_per_launch": slab_b * N * S,
                                     "achieved_gbs": slab_b * N * S / (kt["dw"] / 1e3) / 1e9,

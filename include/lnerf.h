@@ -233,7 +233,8 @@ enum {
     LNERF_PATH_DW16 = 8,      /* dW kernel on wave pairs (dw16_kernel)                        */
     LNERF_PATH_K32 = 16,      /* reserved (k32, removed in round 4)                           */
     LNERF_PATH_K16_W4 = 32,   /* k16 on 4-wave, 64-sample workgroups (two per CU)             */
-    LNERF_PATH_KR = 64        /* the render ran kr (lnerf_render.hip), not k16's forward      */
+    LNERF_PATH_KR = 64,       /* the render ran kr (lnerf_render.hip), not k16's forward      */
+    LNERF_PATH_A24 = 128      /* training kept the activation slabs as int24 (fp16x3)         */
 };
 int lnerf_ctx_last_path(lnerf_ctx* ctx);
 

@@ -475,7 +475,7 @@ struct lnerf_ctx {
 
 static int path_bits(const FusedPlan& p, bool train) {
     return LNERF_PATH_FUSED | LNERF_PATH_K16 | (p.tile == 64 ? LNERF_PATH_K16_W4 : 0) |
-           (train ? LNERF_PATH_DW16 : 0) | (p.x6 << 8);
+           (train ? LNERF_PATH_DW16 : 0) | (train && a24_slabs(p.x6) ? LNERF_PATH_A24 : 0) | (p.x6 << 8);
 }
 
 // Flags that ask for a fused-path kernel or precision: an explicit request that cannot be served

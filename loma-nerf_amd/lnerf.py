@@ -57,6 +57,7 @@ PATH_DW16 = 8
 PATH_K32 = 16      # reserved (k32, removed in round 4)
 PATH_K16_W4 = 32
 PATH_KR = 64       # the render ran kr (lnerf_render.hip)
+PATH_A24 = 128      # training kept the activation slabs as int24 (fp16x3)
 
 
 class LnerfMLP(ctypes.Structure):
@@ -341,7 +342,7 @@ class Engine:
             raise RuntimeError(f"lnerf_ctx_last_path: {last_error()}")
         return dict(generic=bool(v & PATH_GENERIC), fused=bool(v & PATH_FUSED),
                     k16=bool(v & PATH_K16), dw16=bool(v & PATH_DW16), k16_w4=bool(v & PATH_K16_W4),
-                    kr=bool(v & PATH_KR),
+                    kr=bool(v & PATH_KR), a24=bool(v & PATH_A24),
                     planes=(v >> 8) & 3)
 
     def relu_masks(self, L: int, R: int):

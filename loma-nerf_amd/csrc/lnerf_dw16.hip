@@ -1,17 +1,19 @@
 // lnerf_dw16.hip -- k2 on wave pairs: dW_l = sum_s A_{l-1}[s]^T G_l[s] and db_l = sum_s G_l[s]
-// from the slabs k1 wrote, in k1's split (fp16x3 on v_mfma_f32_32x32x16_f16 or bf16x6 on
-// v_mfma_f32_32x32x16_bf16, both with the slabs' layer-wide exponent shifts), two waves per SIMD.
+// from the slabs k1 wrote, in k1's split (fp16x3 on v_mfma_f32_32x32x16_f16, bf16x6 / bf16 on
+// v_mfma_f32_32x32x16_bf16, with per-sample balanced exponent shifts), two waves per SIMD.
 //
 // Reference: the weight/bias adjoints of nerf.py's reverse pass (reverse_diff.py:492-559;
 // dW_l += A_{l-1}^T G_l, db_l += sum_rows G_l). One workgroup (8 waves)
 // streams a contiguous range of 16-sample half-blocks of one layer:
 //  * global -> registers: a slab tile's half-block is sample-major, [feature half 2][16 samples]
-//    [16 features] fp32 (the 1 KiB k1 writes with one global_store_dwordx4 per wave), read as
-//    fully coalesced 16-B loads (4 features of one sample per thread) three half-blocks ahead;
+//    [16 features] (G: fp32, 1 KiB per wave-store of k1; A under fp16x3: int24, 768 B,
+//    lnerf_internal.h a24_slabs), read as fully coalesced 16-B (12-B) loads, 4 features of one
+//    sample per thread, three half-blocks ahead;
 //  * split once, cooperatively: every value is scaled and split into its hi/lo (fp16x3) or
 //    hi/mid/lo (bf16x6) planes exactly once per workgroup and written to a double-buffered LDS
 //    image [plane][16 samples][512 features] (A rows 0..255, G rows 256..511), 8 B per plane and
-//    thread (one ds_write_b64);
+//    thread (one ds_write_b64), the 8-B feature quads XOR-swizzled per sample row (swz) so that
+//    these writes and the fragment reads are both bank-conflict-free;
 //  * MFMA operands come out of that sample-major image transposed by ds_read_b64_tr_b16: lane
 //    (feature l & 31, samples 8 (l >> 5) ..+7) takes two 4-sample x 16-feature blocks;
 //  * each wave owns a TI x TJ block of 32 x 32 output tiles (2 x 4 for the hidden layers);

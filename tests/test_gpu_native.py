@@ -119,14 +119,15 @@ def test_fused_deep_mlp(engine, prec):
     w = _deep(nerf_np.make_workload("cfg2", rays=32, samples=32))
     if prec in FUSED:
         check_fused(engine, w, flags=prec)
+        planes = 3 if prec & lnerf.MFMA_BF16X6 else 2
         assert engine.last_path() == dict(generic=False, fused=True, k16=True, dw16=True, kr=False,
-                                          k16_w4=bool(prec & lnerf.K16_W4),
-                                          planes=3 if prec & lnerf.MFMA_BF16X6 else 2)
+                                          k16_w4=bool(prec & lnerf.K16_W4), planes=planes,
+                                          a24=planes == 2)   # int24 activation slabs under fp16x3
         return
     got = run_native(engine, w, flags=lnerf.FAST | prec)
     # plain bf16 operands (8 significant bits): a loose sanity bound, not the fp32 tolerance
     assert engine.last_path() == dict(generic=False, fused=True, k16=True, dw16=True, kr=False,
-                                      k16_w4=False, planes=1)
+                                      k16_w4=False, planes=1, a24=False)
     want = oracle_ref(w)
     assert abs(got["loss"] - want["loss"]) <= 2e-2 * abs(want["loss"]), (got["loss"], want["loss"])
     assert_close("dW", got["dW"], want["dW"], rtol=0.0, atol_scale=5e-2)
@@ -141,7 +142,7 @@ def test_default_path_is_k16_dw16(engine):
     w = nerf_np.make_workload("cfg3", rays=8)
     run_native(engine, w, per_ray=False)
     assert engine.last_path() == dict(generic=False, fused=True, k16=True, dw16=True, kr=False, k16_w4=False,
-                                      planes=2)
+                                      planes=2, a24=True)
     run_native(engine, w, per_ray=False, flags=lnerf.K16_W4)
     assert engine.last_path()["k16"] and engine.last_path()["k16_w4"]
     run_native(engine, w, per_ray=False, flags=lnerf.MFMA_F16X3)

@@ -560,7 +560,7 @@ def main():
             # k2 streams the slabs k1 wrote: algorithmic bytes = every slab value read once
             # (X, A_l for l < L-1: 3 B per value as int24 under fp16x3 training, else 4; G_l for
             # every l: 4 B; 32-feature tiles)
-            a_b = 3 if t.eng.last_path().get("a24") else 4
+            a_b = 3 if last_path and last_path.get("a24") else 4
             slab_b = 32 * (a_b * (-(-shapes[0][0] // 32) + sum(-(-n // 32) for _, n in shapes[:-1]))
                            + 4 * sum(-(-n // 32) for _, n in shapes))
             out["dw_kernel_hbm"] = {"kernel": "dw16_kernel<2>", "avg_ms": kt["dw"],

@@ -36,6 +36,10 @@ typedef _Float16 hf4 __attribute__((ext_vector_type(4)));
 #ifndef LNERF_DW16_NOMMA
 #define LNERF_DW16_NOMMA 0
 #endif
+// split round k after column k's MFMAs (1): dW 0.733-0.737 -> 0.722-0.726 ms interleaved; 0 = before them
+#ifndef LNERF_DW16_SPLIT_LATE
+#define LNERF_DW16_SPLIT_LATE 1
+#endif
 // half-blocks of slab loads in flight per thread (3: default; 2: 17 fewer registers)
 #ifndef LNERF_DW16_DEPTH
 #define LNERF_DW16_DEPTH 3
@@ -321,7 +325,7 @@ __device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int 
     for (int k = 0; k < 4; ++k) {
         // rows past the layer's tiles are never read: skip their split (wave-uniform: a wave's
         // values of a round lie in one 32-feature tile); FULL layers need no branch
-        if (FULL || m.ok[k]) write_planes_row<PL>(round_values<PL>(nl, k), k, nxt, sa, sg, m);
+        if (!LNERF_DW16_SPLIT_LATE && (FULL || m.ok[k])) write_planes_row<PL>(round_values<PL>(nl, k), k, nxt, sa, sg, m);
         if constexpr (ACTIVE) {
             if (k < TJ) {
                 const int j = k < TJ ? k : 0;
@@ -349,6 +353,7 @@ __device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int 
                 }
             }
         }
+        if (LNERF_DW16_SPLIT_LATE && (FULL || m.ok[k])) write_planes_row<PL>(round_values<PL>(nl, k), k, nxt, sa, sg, m);
     }
 }
 

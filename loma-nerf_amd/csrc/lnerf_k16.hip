@@ -320,7 +320,11 @@ __device__ __forceinline__ bf8 lds_frag(const unsigned char* base) {
 #ifndef LNERF_K16_KDIST
 #define LNERF_K16_KDIST 2
 #endif
-constexpr int kDist = LNERF_K16_KDIST;   // weight tiles read ahead of the one the MFMAs consume
+constexpr int kDist = LNERF_K16_KDIST;
+// where the next k-step's operand split sits among this k-step's output tiles, in quarters
+#ifndef LNERF_K16_SPLIT_AT
+#define LNERF_K16_SPLIT_AT 2
+#endif   // weight tiles read ahead of the one the MFMAs consume
 #ifndef LNERF_K16_SCHED
 #define LNERF_K16_SCHED 1
 #endif
@@ -509,7 +513,7 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
     // first half of the output tiles, [late waves: barrier], the next k-step's operand split (off
     // the next prologue's critical path), second half, [spread: the slab stores, younger than
     // every piece], [early: barrier]
-    constexpr int H = (NTO + 1) / 2;
+    constexpr int H = NTO >= 4 ? NTO * LNERF_K16_SPLIT_AT / 4 : (NTO + 1) / 2;   // split after tile H
     tile_steps<NTO, PL, NW, FD, 0>(std::make_integer_sequence<int, H>{}, base, w, bh, bm, bl, out, job);
     if (late && last) dma_barrier(pending);
     bf8 nh = {}, nm = {}, nl = {};

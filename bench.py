@@ -84,6 +84,8 @@ def parse():
                     help="fwd+bwd only: skip the on-device Adam update (train_nerf.py:133-161) "
                          "that every timed step otherwise applies after the gradient exchange")
     ap.add_argument("--lr", type=float, default=5e-4, help="Adam learning rate (train_nerf.py)")
+    ap.add_argument("--dw-grid", type=int, default=0,
+                    help="dW kernel workgroups per step (lnerf_ctx_set_option OPT_DW_GRID; 0 = default 512)")
     ap.add_argument("--no-render", action="store_true",
                     help="skip the config-5 render record the default N=1 line carries")
     ap.add_argument("--no-cfg2", action="store_true",
@@ -313,6 +315,8 @@ class Trainer:
         self.shapes, wp, bp = scene.init_mlp(3 + 6 * b["F"], 4, b["L"], b["H"])
         self.N, self.S = b["N"], b["S"]
         self.eng = lnerf.Engine(local)
+        if getattr(args, "dw_grid", 0):
+            self.eng.set_option(lnerf.OPT_DW_GRID, args.dw_grid)
         self.mlp = lnerf.make_mlp(self.shapes, wp.shape[1], wp.shape[2])
         # weights and biases packed like the gradient buffer [dW | db], so that one Adam launch
         # updates both (padding entries have zero gradients and never move)

@@ -568,6 +568,10 @@ def main():
             slab_b = 32 * (a_b * (-(-shapes[0][0] // 32) + sum(-(-n // 32) for _, n in shapes[:-1]))
                            + 4 * sum(-(-n // 32) for _, n in shapes))
             out["dw_kernel_hbm"] = {"kernel": "dw16_kernel<2>", "avg_ms": kt["dw"],
+                                    "slab_format": ("int24 activations + f32 gradients" if a_b == 3
+                                                    else "f32 activations + f32 gradients"),
+                                    "note": "issue-bound (split VALU + MFMA per half-block), not HBM-bound: "
+                                            "fewer slab bytes moved it less than in proportion (DESIGN.md §3 k2)",
                                     "bytes_per_sample": slab_b, "bytes_per_launch": slab_b * N * S,
                                     "achieved_gbs": slab_b * N * S / (kt["dw"] / 1e3) / 1e9,
                                     "peak_gbs": PEAK_HBM_GBS,

@@ -321,9 +321,6 @@ __device__ __forceinline__ bf8 lds_frag(const unsigned char* base) {
 #define LNERF_K16_KDIST 2
 #endif
 constexpr int kDist = LNERF_K16_KDIST;
-#ifndef LNERF_K16_EPI_FMA
-#define LNERF_K16_EPI_FMA 0
-#endif
 // where the next k-step's operand split sits among this k-step's output tiles, in quarters
 #ifndef LNERF_K16_SPLIT_AT
 #define LNERF_K16_SPLIT_AT 2
@@ -807,26 +804,12 @@ k16_fwd_bwd_kernel(K16Args a) {
             bias_read<HT>(std::make_integer_sequence<int, HT>{}, bl, bv);
             // values in descending bit order (feature 4o + i ends in bit 4o + i of lo / hi)
             unsigned mlo = 0u, mhi = 0u;
-            // EPI_FMA (A/B): unscale + bias as one fma by 2^sh (bitwise the same as ldexp then add
-            // whenever 2^sh is a float, checked wave-wide)
-            if (LNERF_K16_EPI_FMA && PL >= 2 && __all(sh >= -149 && sh <= 127)) {
-                const float sc = __builtin_ldexpf(1.0f, sh);
 #pragma unroll
-                for (int o = HT - 1; o >= 0; --o) {
+            for (int o = HT - 1; o >= 0; --o) {
 #pragma unroll
-                    for (int i = 3; i >= 0; --i) {
-                        const float v = __builtin_fmaf(out[o][i], sc, bv[o][i]);
-                        act[o][i] = relu_bit(v, o >= 8 ? mhi : mlo);
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int o = HT - 1; o >= 0; --o) {
-#pragma unroll
-                    for (int i = 3; i >= 0; --i) {
-                        const float v = (PL >= 2 ? __builtin_ldexpf(out[o][i], sh) : out[o][i]) + bv[o][i];
-                        act[o][i] = relu_bit(v, o >= 8 ? mhi : mlo);
-                    }
+                for (int i = 3; i >= 0; --i) {
+                    const float v = (PL >= 2 ? __builtin_ldexpf(out[o][i], sh) : out[o][i]) + bv[o][i];
+                    act[o][i] = relu_bit(v, o >= 8 ? mhi : mlo);
                 }
             }
             const unsigned long long mb = ((unsigned long long)mhi << 32) | mlo;

@@ -84,6 +84,9 @@ def parse():
                     help="fwd+bwd only: skip the on-device Adam update (train_nerf.py:133-161) "
                          "that every timed step otherwise applies after the gradient exchange")
     ap.add_argument("--lr", type=float, default=5e-4, help="Adam learning rate (train_nerf.py)")
+    ap.add_argument("--zero-weights", action="store_true",
+                    help="diagnostic only (not a benchmark): all weights and biases zero, to measure how "
+                         "much of the step is the chip's power-limited clock (MI355X_MICROARCH.md DVFS)")
     ap.add_argument("--dw-grid", type=int, default=0,
                     help="dW kernel workgroups per step (lnerf_ctx_set_option OPT_DW_GRID; 0 = default 512)")
     ap.add_argument("--no-render", action="store_true",
@@ -321,6 +324,8 @@ class Trainer:
         # weights and biases packed like the gradient buffer [dW | db], so that one Adam launch
         # updates both (padding entries have zero gradients and never move)
         self.params = torch.cat([torch.from_numpy(wp).reshape(-1), torch.from_numpy(bp).reshape(-1)]).to(dev)
+        if getattr(args, "zero_weights", False):
+            self.params.zero_()
         self.ws = self.params[:wp.size].view(wp.shape)
         self.bs = self.params[wp.size:].view(bp.shape)
         self.adam_m = torch.zeros_like(self.params)

@@ -162,13 +162,24 @@ def sq_counters(kernel, workload, sha):
             "source": src}, None
 
 
-def attach_counters(roof, kernel, workload, sha, with_sq=True):
+def attach_counters(roof, kernel, workload, sha, with_sq=True, work=None):
+    """Counter fields of the committed, hash-matched summaries. `work` (FLOP or bytes per launch,
+    the unit of roof["peak"]): also frac_rocprof = work / the rocprofv3 kernel-trace average of the
+    same library (profiles/*_pmc.json avg_ms, from *_kernel_stats.csv) / peak, and, with SQ
+    counters, frac_at_clock = the HIP-event frac scaled by 2.4 GHz / the SQ-derived clock the
+    kernel ran at under the profiler (the fraction of what the chip's clock allowed)."""
     tr, why = pmc_traffic(kernel, workload, sha)
     if tr:
         roof["traffic"] = tr["bytes"]
         roof["traffic_unit"] = "bytes/launch"
         roof["traffic_source"] = tr["source"]
         roof["traffic_gbs"] = tr["bytes"] / (roof["avg_ms"] / 1e3) / 1e9
+        d, _ = _summaries("pmc", workload, sha)
+        ent = _kernel_entry(d, kernel) if d else None
+        if work is not None and ent and ent.get("avg_ms"):
+            scale = 1e12 if roof.get("unit") == "TFLOP/s" else 1e9
+            roof["avg_ms_rocprof"] = ent["avg_ms"]
+            roof["frac_rocprof"] = work / (ent["avg_ms"] / 1e3) / scale / roof["peak"]
     else:
         roof["traffic_note"] = why
     if with_sq:
@@ -176,6 +187,10 @@ def attach_counters(roof, kernel, workload, sha, with_sq=True):
         if sq:
             roof["mfma_busy"] = sq["mfma_busy"]
             roof["counters"] = sq
+            base = roof.get("kernel_frac", roof.get("frac"))
+            if sq.get("clock_ghz") and base is not None:
+                roof["clock_ghz_profiled"] = sq["clock_ghz"]
+                roof["frac_at_clock"] = base * 2.4 / sq["clock_ghz"]
         else:
             roof["counters_note"] = why
 
@@ -465,8 +480,8 @@ def bench_render(args, world, rank, local, dist, steps=None, warmup=None):
             roof["avg_ms"] = kern_ms
             roof["kernel_achieved"] = fwd_flops * N * S / (kern_ms / 1e3) / 1e12
             roof["kernel_frac"] = roof["kernel_achieved"] / peak
-            if not args.x6 and world == 1:
-                attach_counters(roof, kernel, "cfg5", lib_sha16())
+            if not args.x6 and not getattr(args, "render_k16", False) and world == 1:
+                attach_counters(roof, kernel, "cfg5", lib_sha16(), work=fwd_flops * N * S)
         rec = {
             "metric": "ray-samples/sec fwd (eval render), 800x800 frame x 128 samples",
             "value": total / (ms / 1e3), "unit": "ray-samples/s", "n_gpus": world,
@@ -477,6 +492,7 @@ def bench_render(args, world, rank, local, dist, steps=None, warmup=None):
             "config": {"workload": "cfg5: 800x800 rays x 128 samples per frame, PE F=5, "
                                    "MLP 33->256x7->4, forward only",
                        "rays_per_gpu": N, "parallelism": f"replicas{world}",
+                       "variant": [v for v in ("x6", "render-k16") if getattr(args, v.replace("-", "_"), False)] or None,
                        "gather": ("the whole frame's colours all-gathered on every rank inside the "
                                   "timed step (dp.gather_rows)" if world > 1 else None)},
             "roofline": roof,
@@ -485,11 +501,67 @@ def bench_render(args, world, rank, local, dist, steps=None, warmup=None):
     return rec
 
 
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv, cmd=None, env=None) -> int:
+    """`bench.py --gpus N` outside torchrun: start N rank processes of this same command (one per
+    GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set per child, rendezvous on
+    127.0.0.1) and wait for all of them. Called before anything touches the GPU (this process never
+    initialises HIP; the ranks are children, nothing is exec'd). Rank 0 prints the JSON line.
+    Returns the first non-zero exit status (a rank that fails makes the launch fail), else 0."""
+    import subprocess
+    cmd = cmd or [sys.executable, os.path.abspath(__file__)]
+    base = dict(os.environ if env is None else env)
+    base.setdefault("MASTER_ADDR", "127.0.0.1")
+    base.setdefault("MASTER_PORT", str(free_port()))
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n))
+        procs.append(subprocess.Popen(cmd + list(argv), env=e))
+    rcs = [p.wait() for p in procs]
+    return next((rc for rc in rcs if rc != 0), 0)
+
+
+def variant_flags(args) -> list:
+    """Every non-default measurement mode of this run: a bench line that carries any of them is not
+    the headline configuration, says so in config.variant / data, and attaches no counters
+    (those were profiled on the default configuration)."""
+    v = []
+    for name in ("zero_weights", "generic", "x6_train", "k16_w4", "no_optimizer", "strong", "render_k16", "x6"):
+        if getattr(args, name, False):
+            v.append(name.replace("_", "-"))
+    if getattr(args, "dw_grid", 0):
+        v.append(f"dw-grid={args.dw_grid}")
+    if getattr(args, "input", "rays") != "rays":
+        v.append(f"input={args.input}")
+    if getattr(args, "rays", None):
+        v.append(f"rays={args.rays}")
+    if getattr(args, "config", "cfg3") != "cfg3":
+        v.append(f"config={args.config}")
+    if os.environ.get("LNERF_LIB"):
+        v.append(f"lib={os.path.basename(os.environ['LNERF_LIB'])}")
+    return v
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU, started here (before any HIP call) instead of by torchrun
+        raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report n_gpus={world}")
     import torch
     import scene
 
@@ -521,16 +593,22 @@ def main():
     last_path = None if args.generic else t.eng.last_path()
     t.close()
 
+    variants = variant_flags(args)
     if rank == 0:
         out = {
-            "metric": METRIC, "value": value, "unit": "ray-samples/s", "n_gpus": world,
+            "metric": (METRIC if not args.zero_weights else
+                       "DIAGNOSTIC (not a benchmark: all-zero weights, DVFS check): " + METRIC),
+            "value": value, "unit": "ray-samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
             "higher_is_better": True, "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None, "dtype": "f32",
             "mfma": ("generic (no MFMA)" if args.generic else
                      "bf16x6 (fp32 operands split hi+mid+lo, fp32 accumulate)" if args.x6_train else
                      "fp16x3 (fp32 operands x 2^e split hi+lo in fp16, 3 products, fp32 accumulate)"),
-            "data": "synthetic (look-at camera rays, uniform targets, random-init MLP seed 215)",
+            "data": ("synthetic (look-at camera rays, uniform targets, random-init MLP seed 215)"
+                     if not args.zero_weights else
+                     "synthetic rays and targets, ALL-ZERO weights and biases (--zero-weights diagnostic)")
+                    + ("" if not variants else f"; non-default run: {', '.join(variants)}"),
             "config": {"workload": (f"cfg4 (strong): one {total_rays}-ray x {S}-sample batch sharded "
                                     f"over {world} GPU(s), {N} rays on rank 0" if args.strong else
                                     f"{args.config}: {N} rays x {S} samples per GPU")
@@ -540,10 +618,13 @@ def main():
                        "optimizer": (None if args.no_optimizer else
                                      f"adam lr {args.lr} on device (train_nerf.py:133-161), in the step"),
                        "input": ("rays: sampling, dists and positional encoding on the GPU"
-                                 if args.input == "rays" else "points: sampled on the host")},
+                                 if args.input == "rays" else "points: sampled on the host"),
+                       "variant": variants or None},
+            "diagnostic": bool(args.zero_weights),
             "step_tflops": step_flops / (ms / 1e3) / 1e12,
             "host_enqueue_ms_per_step": t_host / args.steps * 1e3,
             "lib_sha16": lib_sha16(),
+            "build_knobs": __import__("lnerf").build_knobs(),
         }
         if kt:
             fus_ms = kt["fused"]
@@ -560,8 +641,8 @@ def main():
                                    "fp32-accurate multiply-add)" if args.x6_train
                                    else "fp16 MFMA dense 2516.6 TF / 3 (fp16x3: three fp16 "
                                    "products per multiply-add)")}
-            if args.rays is None and not args.strong and args.config == "cfg3" and not args.x6_train:
-                attach_counters(roof, k1, "cfg3", out["lib_sha16"])
+            if not variants:
+                attach_counters(roof, k1, "cfg3", out["lib_sha16"], work=fused_flops)
             out["roofline"] = roof
             out["kernels_ms"] = kt
             out["dw_kernel_tflops"] = dw_flops / (kt["dw"] / 1e3) / 1e12
@@ -581,9 +662,12 @@ def main():
                                     "achieved_gbs": slab_b * N * S / (kt["dw"] / 1e3) / 1e9,
                                     "peak_gbs": PEAK_HBM_GBS,
                                     "frac": slab_b * N * S / (kt["dw"] / 1e3) / 1e9 / PEAK_HBM_GBS}
-            if args.rays is None and not args.strong and args.config == "cfg3" and not args.x6_train:
-                attach_counters(out["dw_kernel_hbm"], "dw16_kernel<2>", "cfg3", out["lib_sha16"])
-        extras = world == 1 and not (args.generic or args.strong or args.rays) and args.config == "cfg3"
+            if not variants:
+                out["dw_kernel_hbm"]["unit"] = "GB/s"
+                out["dw_kernel_hbm"]["peak"] = PEAK_HBM_GBS
+                attach_counters(out["dw_kernel_hbm"], "dw16_kernel<2>", "cfg3", out["lib_sha16"],
+                                work=slab_b * N * S)
+        extras = world == 1 and not variants
         if extras and not args.no_cfg2:
             out["config2"] = bench_config2(args, local)
         if extras and not args.no_render:

@@ -192,6 +192,11 @@ typedef struct {
 
 const char* lnerf_last_error(void);
 const char* lnerf_version(void);
+/* Build fingerprint: a bitmask of the kernel objects' compile-time knobs (k1 / k2 scheduling, the
+   int24 slab format, the phase-profiling build) that differ from the product build. 0 for the
+   shipped library; A/B variants (Makefile defvariant / dwdefvariant) report what they moved.
+   No reference counterpart (engine-only). */
+unsigned lnerf_build_knobs(void);
 
 int lnerf_ctx_create(lnerf_ctx** out, int device);
 void lnerf_ctx_destroy(lnerf_ctx* ctx);

@@ -32,10 +32,6 @@ typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
 typedef _Float16 hf8 __attribute__((ext_vector_type(8)));
 typedef _Float16 hf4 __attribute__((ext_vector_type(4)));
 
-// timing experiments only (wrong results): skip the MFMAs / the slab loads
-#ifndef LNERF_DW16_NOMMA
-#define LNERF_DW16_NOMMA 0
-#endif
 // split round k after column k's MFMAs (1): dW 0.733-0.737 -> 0.722-0.726 ms interleaved; 0 = before them
 #ifndef LNERF_DW16_SPLIT_LATE
 #define LNERF_DW16_SPLIT_LATE 1
@@ -134,12 +130,19 @@ struct Loads {
 // D = exA + exG - E_l -- a sample whose A is tiny and G huge (tiny sigma behind the 1e8 delta)
 // no longer pushes every other sample's G toward fp16's subnormals. Neither operand exceeds its
 // own ideal shift, so nothing overflows. -128 marks an all-zero row: its partner keeps its own
-// shift (the zero products stay zero).
+// shift (the zero products stay zero). kSexpNonFinite marks an activation row holding a NaN or an
+// infinity (k1 store_sexp, encoded at shift 0): its G row keeps its own shift and the A row takes
+// the rest of E, so the product scale stays 2^E; its terms are non-finite anyway.
 __device__ __forceinline__ void sample_shifts(unsigned e, int E, int& ea, int& eg) {
     const int xa = (int)(signed char)(e & 0xFFu), xg = (int)(signed char)(e >> 8);
     if (xa == -128 || xg == -128) {
-        ea = xa == -128 ? 0 : xa;
+        ea = xa < -126 ? 0 : xa;
         eg = xg == -128 ? 0 : xg;
+        return;
+    }
+    if (xa == kSexpNonFinite) {
+        eg = xg;
+        ea = E - xg;
         return;
     }
     const int d = xa + xg - E;   // >= 0
@@ -248,16 +251,28 @@ __device__ __forceinline__ void sample_scales(unsigned e, int E, float& sa, floa
     sample_shifts(e, E, ea, eg);
     if constexpr (a24_slabs(PL)) {
         const int xa = (int)(signed char)(e & 0xFFu);
-        ea = xa == -128 ? 0 : ea - xa - 8;
+        ea = xa == -128 ? 0 : ea - (xa == kSexpNonFinite ? 0 : xa) - 8;
     }
     sa = __builtin_ldexpf(1.0f, ea);
     sg = __builtin_ldexpf(1.0f, eg);
 }
 
-// round i's values as the split takes them (int24 A rounds decoded)
+// round i's values as the split takes them (int24 A rounds decoded). A row k1 marked non-finite
+// (kSexpNonFinite) turns its out-of-range codes (|q| >= 2^22: NaN and +-infinity) back into NaN;
+// the test is one wave-uniform branch, taken only when some lane's sample is marked.
 template <int PL>
 __device__ __forceinline__ fx4 round_values(const Loads& L, int i) {
-    if constexpr (a24_slabs(PL)) return i < 2 ? decode_a24(L.v[i]) : L.v[i];
+    if constexpr (a24_slabs(PL)) {
+        if (i >= 2) return L.v[i];
+        fx4 v = decode_a24(L.v[i]);
+        const bool marked = (int)(signed char)(L.e & 0xFFu) == kSexpNonFinite;
+        if (__builtin_amdgcn_ballot_w64(marked)) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (marked && __builtin_fabsf(v[j]) >= 4194304.0f) v[j] = __builtin_nanf("");
+        }
+        return v;
+    }
     return L.v[i];
 }
 
@@ -431,7 +446,7 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
     const int KT = a.kt[l], NT = a.nt[l];
     const int nbg = (NT + TJ - 1) / TJ, nblk = ((KT + TI - 1) / TI) * nbg;
-    const bool active = wave < nblk && !LNERF_DW16_NOMMA;
+    const bool active = wave < nblk;
     const int a0 = active ? (wave / nbg) * 32 * TI : 0, g0 = active ? (wave % nbg) * 32 * TJ : 0;
     // half-block range of this split
     const int hbs = 2 * a.blocks, splits = a.splits[l];
@@ -585,6 +600,12 @@ __global__ void __launch_bounds__(1024) k1_reduce_kernel(const int* __restrict__
 }
 
 }  // namespace
+
+// compile-time settings of this object that differ from the product build (lnerf_build_knobs)
+unsigned dw16_build_knobs() {
+    return (LNERF_DW16_SPLIT_LATE != 1 ? kKnobDwSplitLate : 0u) | (LNERF_DW16_DEPTH != 3 ? kKnobDwDepth : 0u) |
+           (LNERF_DW16_SWZ != 1 ? kKnobDwSwz : 0u) | (LNERF_A24 != 1 ? kKnobA24 : 0u);
+}
 
 void dw16_launch(const FusedPlan& p, hipStream_t s) {
     Dw16Args a{};

@@ -55,7 +55,21 @@ __device__ __forceinline__ void split_h2(float x0, float x1, float sc, unsigned&
 #define LNERF_A24 1
 #endif
 __host__ __device__ constexpr bool a24_slabs(int PL) { return PL == 2 && LNERF_A24 != 0; }
+// k1's shift byte of an activation row holding a NaN or an infinity (its max is non-finite): the row
+// is encoded at shift 0, and dw16 decodes its out-of-range codes (|q| >= 2^22: +-inf leaves 2^22,
+// NaN 1.5 2^23) as NaN, so a non-finite activation still makes its dW terms non-finite
+constexpr int kSexpNonFinite = -127;
 __host__ __device__ constexpr int a_tile_floats(int PL) { return a24_slabs(PL) ? 768 : 1024; }
+
+// ---- build fingerprint (lnerf_build_knobs): one bit per compile-time knob of the kernel objects
+// set away from the product default. The shipped library reports 0; tests and bench.py record it.
+enum : unsigned {
+    kKnobK16FullDma = 1u << 0, kKnobK16KDist = 1u << 1, kKnobK16SplitAt = 1u << 2, kKnobK16Sched = 1u << 3,
+    kKnobK16Prio = 1u << 4, kKnobK16Spread = 1u << 5, kKnobProf = 1u << 6, kKnobA24 = 1u << 7,
+    kKnobK16Only = 1u << 8, kKnobDwSplitLate = 1u << 9, kKnobDwDepth = 1u << 10, kKnobDwSwz = 1u << 11,
+};
+unsigned k16_build_knobs();
+unsigned dw16_build_knobs();
 
 // ---- ray sampling (train_nerf.py:289-306), float64 as numpy computes it -----------------------
 // t_j = np.linspace(near, far, S)[j]: j * ((far - near) / (S - 1)) + near, the last one = far.

@@ -43,23 +43,6 @@ constexpr int kWaves = 8;                     // the most waves per workgroup
 constexpr int kMaxChunks = 2 * kMaxLayers * 8 + 1;   // <= 2 passes x 8 k-steps per layer + 1 end
 constexpr int kMaxT = 16;                     // 16-feature tiles per 256-wide layer
 constexpr int kCompBytes = 2688 * 4;          // composite_tile's scratch (comp[0, 2688))
-// timing experiments only (wrong results): drop the slab stores / the weight DMA after chunk 2
-#ifndef LNERF_K16_NOSTORE
-#define LNERF_K16_NOSTORE 0
-#endif
-#ifndef LNERF_K16_NODMA
-#define LNERF_K16_NODMA 0
-#endif
-#ifndef LNERF_K16_NOBAR
-#define LNERF_K16_NOBAR 0
-#endif
-// timing experiments only (wrong results): no encoding sincos / no compositing
-#ifndef LNERF_K16_NOPE
-#define LNERF_K16_NOPE 0
-#endif
-#ifndef LNERF_K16_NOCOMP
-#define LNERF_K16_NOCOMP 0
-#endif
 // full hidden passes get compile-time step bounds and test-free DMA issue (A/B: 0 = generic only)
 #ifndef LNERF_K16_FULLDMA
 #define LNERF_K16_FULLDMA 1
@@ -244,9 +227,7 @@ __device__ __forceinline__ void dma_barrier(int pending) {
     else if (pending > 0) vm_wait_n(pending, std::make_integer_sequence<int, 64>{});
     PROF_ADD(kPfVm, t0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#if !LNERF_K16_NOBAR   // timing experiment only (wrong results): no chunk barrier
     __builtin_amdgcn_s_barrier();
-#endif
     asm volatile("" ::: "memory");
     PROF_ADD(kPfBar, t0);
 }
@@ -297,7 +278,9 @@ __device__ __forceinline__ void store_slab_step(float* __restrict__ dst, const f
 // global_store_dwordx3 into the 1.5-KiB half-block run [feature half 2][16 samples][16 f] x 3 B.
 __device__ __forceinline__ void store_slab_step24(unsigned char* __restrict__ dst, const fx4& t0, const fx4& t1,
                                                   int ex) {
-    typedef unsigned u3 __attribute__((ext_vector_type(3)));
+    // 4-byte aligned (the 12-B runs sit at 12 g): a plain 3-vector claims 16-B size and alignment,
+    // which would let the compiler widen the store over the neighbouring lane's bytes
+    typedef unsigned u3 __attribute__((ext_vector_type(3), aligned(4)));
     const int lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
     constexpr float kMagic = 12582912.0f;   // 1.5 2^23
     auto pack = [&](const fx4& t) {
@@ -329,18 +312,10 @@ constexpr int kDist = LNERF_K16_KDIST;
 #define LNERF_K16_SCHED 1
 #endif
 
-// timing experiments only (wrong results): read one plane per tile / skip the operand split
-#ifndef LNERF_K16_HALFLDS
-#define LNERF_K16_HALFLDS 0
-#endif
-#ifndef LNERF_K16_NOSPLIT
-#define LNERF_K16_NOSPLIT 0
-#endif
 template <int PL, int O>
 __device__ __forceinline__ void read_tile(const unsigned char* base, bf8 (&w)[3]) {
     w[0] = lds_frag<(O * PL + 0) * 1024>(base);
-    if constexpr (PL >= 2 && LNERF_K16_HALFLDS) w[1] = w[0];
-    else if constexpr (PL >= 2) w[1] = lds_frag<(O * PL + 1) * 1024>(base);
+    if constexpr (PL >= 2) w[1] = lds_frag<(O * PL + 1) * 1024>(base);
     if constexpr (PL == 3) w[2] = lds_frag<(O * PL + 2) * 1024>(base);
 }
 
@@ -417,7 +392,7 @@ __device__ __forceinline__ void tile_steps(std::integer_sequence<int, O...>, con
 // bf16x6 hi/mid/lo, fp16x3 hi/lo (x 2^ex), or plain bf16.
 template <int PL>
 __device__ __forceinline__ void make_b(const fx4 (&in)[kMaxT], int s, int ex, bf8& bh, bf8& bm, bf8& bl) {
-    if constexpr (PL == 2 && !LNERF_K16_NOSPLIT) {
+    if constexpr (PL == 2) {
         typedef unsigned u4 __attribute__((ext_vector_type(4)));
         u4 hv, lv;
         const float sc = __builtin_ldexpf(1.0f, ex);
@@ -442,9 +417,6 @@ __device__ __forceinline__ void make_b(const fx4 (&in)[kMaxT], int s, int ex, bf
                 bh[j] = h;
                 bm[j] = m;
                 bl[j] = l;
-            } else if (PL == 2) {   // LNERF_K16_NOSPLIT timing experiment
-                bh[j] = __builtin_bit_cast(__bf16, (_Float16)x);
-                bm[j] = bh[j];
             } else {
                 bh[j] = (__bf16)x;
             }
@@ -467,7 +439,7 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
     using R = Ring<PL, NW>;
     const int lane = threadIdx.x & 63;
     const unsigned char* base = ring + (ci % R::slots) * R::slot_bytes + kk * NTO * PL * 1024 + lane * 16;
-    const bool st = slab && !LNERF_K16_NOSTORE;
+    const bool st = slab != nullptr;
     constexpr bool spread = LNERF_K16_SPREAD && !R::stagger;
     DmaJob job;
     if (kk == 0) {
@@ -476,7 +448,7 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
         // now, before the first weight tiles; spread: one piece per kPiecesMax-th of the output
         // tiles, between the MFMAs. The barrier waits for this wave's pieces of chunk ci + 1 only:
         // the slab stores issued after them (two per k-step) stay in flight.
-        const ChunkT c = (LNERF_K16_NODMA && ci >= 2) ? ChunkT{nullptr, 0, -1} : chunk_at(a, ci + 1);
+        const ChunkT c = chunk_at(a, ci + 1);
         unsigned char* dst = ring + ((ci + 1) % R::slots) * R::slot_bytes;
         int issued;
         if constexpr (spread) {
@@ -595,14 +567,21 @@ __device__ __forceinline__ void k16_pass_n(const K16Args& a, int ks, int& ci, un
 
 // The per-sample max|x| of a pass's input (lanes n, n + 16, n + 32, n + 48 hold sample n's
 // features), the basis of its exponent shift (PL >= 2) and of dw16's balancing (training).
+// KEEP_NAN (activation rows, the forward): NaN-propagating (v_maximum3_f32), so a row holding a NaN
+// or an infinity has a non-finite maximum, which store_sexp marks for dw16 (an int24 slab cannot
+// carry the value itself; such a row's pre-activations are NaN and its G row is 0 past the ReLU).
+// Otherwise (gradient rows, the reverse chain) NaN-dropping: loma's sigmoid adjoint puts NaN into
+// an rgb column (nerf.py:157-165) while the row's finite values still need their own shift.
+template <bool KEEP_NAN>
 __device__ __forceinline__ float sample_max(const fx4 (&in)[kMaxT]) {
+    auto mx = [](float a, float b) { return KEEP_NAN ? __builtin_elementwise_maximum(a, b) : __builtin_fmaxf(a, b); };
     float m = 0.0f;
 #pragma unroll
     for (int o = 0; o < kMaxT; ++o)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) m = __builtin_fmaxf(m, __builtin_fabsf(in[o][i]));
-    m = __builtin_fmaxf(m, __shfl_xor(m, 16));
-    return __builtin_fmaxf(m, __shfl_xor(m, 32));
+        for (int i = 0; i < 4; ++i) m = mx(m, __builtin_fabsf(in[o][i]));
+    m = mx(m, __shfl_xor(m, 16));
+    return mx(m, __shfl_xor(m, 32));
 }
 
 // the exponent shift ex with m 2^ex in [2^13, 2^14) (fp16x3_shift)
@@ -614,7 +593,10 @@ __device__ __forceinline__ int shift_of(float m) { return fp16x3_shift(m); }
 // Returns the byte.
 __device__ __forceinline__ int store_sexp(const K16Args& a, int l, int which, float m) {
     const int lane = threadIdx.x & 63;
-    const int x = m > 0.0f ? shift_of(m) : -128;
+    // -128: an all-zero row; -127 (activation rows only): a row with a non-finite value, int24-encoded
+    // at shift 0, whose NaN / infinity codes dw16 turns back into NaN (kSexpNonFinite)
+    const bool fin = m < __builtin_inff();
+    const int x = (m > 0.0f && fin) ? shift_of(m) : (which == 0 && !(m == 0.0f)) ? kSexpNonFinite : -128;
     if (lane < 16) {
         const int p = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + lane;
         a.sexp[((size_t)l * a.rpad + p) * 2 + which] = (signed char)x;
@@ -645,7 +627,7 @@ struct ExPack {
 // marked -128 excluded), one plain store per wave into epart[l][global wave]; k1_reduce_kernel
 // folds them into dw16's per-layer product shift E_l.
 __device__ __forceinline__ void store_emin(const K16Args& a, int l, int xa, int xg) {
-    int v = (xa == -128 || xg == -128) ? (1 << 20) : xa + xg;
+    int v = (xa < -126 || xg < -126) ? (1 << 20) : xa + xg;
 #pragma unroll
     for (int d = 1; d < 16; d <<= 1) v = min(v, __shfl_xor(v, d));
     if ((threadIdx.x & 63) == 0)
@@ -739,12 +721,7 @@ k16_fwd_bwd_kernel(K16Args a) {
                 pe[sl * kStride + c] = (float)xc;
             } else {
                 double sn, cs;
-#if LNERF_K16_NOPE   // timing experiment only (wrong results): no float64 sincos
-                sn = xc;
-                cs = xc;
-#else
                 sincos(ldexp(xc, q - 1), &sn, &cs);
-#endif
                 pe[sl * kStride + 3 + 6 * (q - 1) + c] = (float)sn;
                 pe[sl * kStride + 6 + 6 * (q - 1) + c] = (float)cs;
             }
@@ -790,7 +767,7 @@ k16_fwd_bwd_kernel(K16Args a) {
                                 half * (AT / 2);
         zero_tiles(out);
         const float* bl = bias_ring + (l % 3) * 256 + g * 4;
-        const float xm = (PL >= 2 || st) ? sample_max(act) : 0.0f;
+        const float xm = (PL >= 2 || st) ? sample_max<true>(act) : 0.0f;
         if (st) exa.put(l, store_sexp(a, l, 0, xm));
         const int ex = shift_of(xm);
         const int sh = unscale(l, ex);
@@ -832,7 +809,7 @@ k16_fwd_bwd_kernel(K16Args a) {
 
     // ---- rendering + loss + rendering reverse (one thread per sample, scans along rays) ----
     if (a.head_fit) comp::fit_tile(a, wg, comp, rayloss, st, a.nout);
-    else if (!LNERF_K16_NOCOMP) comp::composite_tile(a, wg, comp, rayloss, st);
+    else comp::composite_tile(a, wg, comp, rayloss, st);
     __syncthreads();
     if (tid == 0) {
         float lsum = 0.0f;
@@ -854,7 +831,7 @@ k16_fwd_bwd_kernel(K16Args a) {
         float* slab = a.grad + a.grad_off[l] + blk * (size_t)(a.nt[l] * 1024) + half * 512;
         PROF_T(t_b);
         const unsigned long long mb = mask_w[(size_t)(l - 1) * NW * 64];   // in flight over the pass
-        const float xm = sample_max(act);
+        const float xm = sample_max<false>(act);
         store_emin(a, l, exa.get(l), store_sexp(a, l, 1, xm));
         const int ex = shift_of(xm);
         const int sh = unscale(l, ex);
@@ -879,7 +856,7 @@ k16_fwd_bwd_kernel(K16Args a) {
     if (a.d_x) {
         // d_layer_input = G_0 W_0^T (ENCODED mode); the pass also writes G_0's slab
         zero_tiles(out);
-        const float xm = sample_max(act);
+        const float xm = sample_max<false>(act);
         store_emin(a, 0, exa.get(0), store_sexp(a, 0, 1, xm));
         const int ex = shift_of(xm);
         const int sh = unscale(0, ex);
@@ -896,7 +873,7 @@ k16_fwd_bwd_kernel(K16Args a) {
                 }
         }
     } else {
-        store_emin(a, 0, exa.get(0), store_sexp(a, 0, 1, sample_max(act)));
+        store_emin(a, 0, exa.get(0), store_sexp(a, 0, 1, sample_max<false>(act)));
 #pragma unroll
         for (int s = 0; s < 8; ++s)
             if (s < a.ks_b[0]) store_slab_step(g0 + s * 1024, act[2 * s], act[2 * s + 1]);
@@ -1018,6 +995,19 @@ __global__ void k16_masks_kernel(const unsigned long long* __restrict__ mask_g, 
 }
 
 }  // namespace
+
+// Compile-time settings of this object that differ from the product build (lnerf_build_knobs):
+// 0 for the shipped library; an A/B variant built with -D... reports which knob it moved.
+unsigned k16_build_knobs() {
+    return (LNERF_K16_FULLDMA != 1 ? kKnobK16FullDma : 0u) | (LNERF_K16_KDIST != 2 ? kKnobK16KDist : 0u) |
+           (LNERF_K16_SPLIT_AT != 2 ? kKnobK16SplitAt : 0u) | (LNERF_K16_SCHED != 1 ? kKnobK16Sched : 0u) |
+           (LNERF_K16_PRIO != 0 ? kKnobK16Prio : 0u) | (LNERF_K16_SPREAD != 1 ? kKnobK16Spread : 0u) |
+           (LNERF_PROF != 0 ? kKnobProf : 0u) | (LNERF_A24 != 1 ? kKnobA24 : 0u)
+#ifdef LNERF_K16_ONLY_16_2
+           | kKnobK16Only
+#endif
+        ;
+}
 
 void k16_masks_launch(const FusedPlan& p, unsigned char* out, hipStream_t s) {
     const size_t n = (size_t)(p.L - 1) * p.R * 32;

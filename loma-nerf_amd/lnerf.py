@@ -46,7 +46,7 @@ EXPORTED_SYMBOLS = [
     "mult_a_b", "lnerf_last_error", "lnerf_version", "lnerf_ctx_create", "lnerf_ctx_destroy",
     "lnerf_workspace_bytes", "lnerf_train_step", "lnerf_render", "lnerf_scale_by_device_scalar",
     "lnerf_adam_update", "lnerf_ctx_timings", "lnerf_get_rays", "lnerf_ctx_last_path",
-    "lnerf_ctx_set_option", "lnerf_ctx_relu_masks",
+    "lnerf_ctx_set_option", "lnerf_ctx_relu_masks", "lnerf_build_knobs",
 ]
 
 # lnerf_ctx_last_path bits
@@ -143,6 +143,8 @@ def configure(lib: ctypes.CDLL) -> None:
     lib.mult_a_b.restype = None
     lib.lnerf_last_error.restype = ctypes.c_char_p
     lib.lnerf_version.restype = ctypes.c_char_p
+    lib.lnerf_build_knobs.argtypes = []
+    lib.lnerf_build_knobs.restype = ctypes.c_uint
     lib.lnerf_ctx_create.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int]
     lib.lnerf_ctx_destroy.argtypes = [ctypes.c_void_p]
     lib.lnerf_ctx_destroy.restype = None
@@ -169,6 +171,11 @@ def configure(lib: ctypes.CDLL) -> None:
                  "lnerf_ctx_create", "lnerf_train_step", "lnerf_render",
                  "lnerf_scale_by_device_scalar", "lnerf_adam_update", "lnerf_get_rays"):
         getattr(lib, name).restype = ctypes.c_int
+
+
+def build_knobs() -> int:
+    """lnerf_build_knobs(): non-default compile-time knobs of the loaded library (0 = product)."""
+    return int(load_library().lnerf_build_knobs())
 
 
 def last_error() -> str:

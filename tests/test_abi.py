@@ -40,6 +40,21 @@ def test_library_exports_every_header_symbol():
     assert lib.lnerf_version().decode().startswith("loma-nerf-amd")
 
 
+def test_shipped_library_is_knob_free():
+    """The library the product path loads was built with every compile-time knob at its product
+    default (lnerf_build_knobs() == 0): no A/B or phase-profiling variant is installed as
+    lib/libloma_nerf.so (the wrong-result timing knobs no longer exist in the sources)."""
+    if os.environ.get("LNERF_LIB"):
+        pytest.skip("LNERF_LIB selects a variant library on purpose")
+    assert lnerf.build_knobs() == 0
+    csrc = os.path.join(REPO, "loma-nerf_amd", "csrc")
+    for f in os.listdir(csrc):
+        if f.endswith((".hip", ".h", ".cpp")):
+            src = open(os.path.join(csrc, f)).read()
+            for knob in ("NOSTORE", "NODMA", "NOBAR", "NOPE", "NOCOMP", "HALFLDS", "NOSPLIT", "NOMMA"):
+                assert f"LNERF_K16_{knob}" not in src and f"LNERF_DW16_{knob}" not in src, (f, knob)
+
+
 def test_library_is_gfx950_code_object():
     # the fat binary embeds the offload target triple of its code object(s)
     blob = open(lnerf.LIB_PATH, "rb").read()

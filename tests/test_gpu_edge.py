@@ -155,3 +155,81 @@ def test_edge_numerics(engine, name, prec):
     if not want_nan:
         assert sub.any()
     assert (np.sign(got["d_dists"][sub]) == np.sign(g["d_dists"][sub])).all()
+
+
+@pytest.mark.parametrize("prec", list(PRECS))
+def test_nan_input_row_propagates(engine, prec):
+    """a NaN in the encoded input (ENCODED mode, the loma layer_input) must leave dW
+    non-finite exactly where the float64 restatement's is. ReLU turns the NaN pre-activations
+    into 0 (nerf.py:141-144: z > 0 is false), so the loss and every other output stay finite, and
+    dW_0[k, :] = X[s, k] G_0[s, :] = NaN * 0 = NaN for the NaN input features only. fp16x3 training
+    keeps activation slabs as int24, which cannot hold a NaN: k1 marks the row (kSexpNonFinite) and
+    k2 decodes its NaN code back to NaN."""
+    import lnerf
+    import nerf_np
+    w = nerf_np.make_workload("cfg2", rays=24, samples=16)
+    X = w.X.copy()
+    X[5, 7] = np.nan
+    X[200, 0] = np.nan
+    shapes = [x.shape for x in w.ws]
+    g = dict(X=X, wp=w.wp, bp=w.bp, dists=w.dists, target=w.target, S=w.S, shapes=np.array(shapes))
+    got, path = run(engine, g, PRECS[prec])
+    if prec == "fp16x3":
+        assert path["a24"], path
+    with np.errstate(all="ignore"):
+        r = nerf_np.nerf_forward_backward(X, w.ws, w.bs, w.dists, w.target, w.S, seed=1.0)
+    assert np.isfinite(r["loss"]) and np.isfinite(got["loss"])
+    for l, (k, n) in enumerate(shapes):
+        want = r["dW"][l]
+        assert np.array_equal(np.isnan(got["dW"][l, :k, :n]), np.isnan(want)), (l, prec)
+        fin = np.isfinite(want)
+        scale = np.abs(np.where(fin, want, 0)).max()
+        err = np.abs(np.where(fin, got["dW"][l, :k, :n] - want, 0))
+        assert (err <= 1e-5 * np.abs(np.where(fin, want, 0)) + 1e-5 * scale).all(), (l, prec, float(err.max()))
+    assert np.isnan(r["dW"][0][7]).all() and np.isnan(r["dW"][0][0]).all()
+    close_grouped("acc", got["acc"], r["acc"])
+
+
+def test_tiny_sigma_delta_1e8_at_bench_size(engine):
+    """the delta = 1e8 / tiny-sigma pattern of edge_finite_6x8 injected into
+    a bench-sized batch (2048 rays x 64 samples, the cfg3 MLP 33->256x7->4, fp16x3 default): the
+    head's sigma column is scaled by 1e-8 and its bias set to 1e-9, so every sample's sigma is
+    0 or ~1e-9, the last sample of every ray (delta = 1e8, train_nerf.py:306-311) has alpha ~ 0.1
+    and a dsigma ~ 1e8 g_alpha, and every other sample's rgb gradient is ~alpha ~ 1e-10 of its
+    sigma gradient -- the head G rows span 2^30, as in the fixture. Against float64 at the GPU's
+    ReLU decisions, with NO a-priori-bound term: every output within 1e-5, every dW column within
+    1e-4 of its own maximum."""
+    import nerf_np
+    from fused_parity import FLIP_MARGIN, encoded_input, padded, run_fused
+    from loma_calls import assert_close
+    w = nerf_np.make_workload("cfg3", rays=2048)
+    ws = [x.copy() for x in w.ws]
+    bs = [x.copy() for x in w.bs]
+    ws[-1][:, 3] *= 1e-8
+    bs[-1][3] = 1e-9
+    wp, bp = nerf_np.pad_weights(ws, bs)
+    w = nerf_np.Workload(w.pts, w.pts32, w.X, w.dists, w.target, ws, bs, wp, bp, w.F, w.S, w.N)
+    got = run_fused(engine, w, seed=1.0)
+    X = encoded_input(w, True)
+    ref = nerf_np.nerf_forward_backward_chunked(X, ws, bs, w.dists, w.target, w.S, seed=1.0,
+                                                masks=got["masks"], rays_per_chunk=256)
+    sig_frac = None
+    tol = dict(rtol=1e-5, atol_scale=1e-5)
+    assert abs(got["loss"] - ref["loss"]) <= 1e-6 * ref["loss"]
+    assert_close("acc", got["acc"], ref["acc"], **tol)
+    assert_close("d_dists", got["d_dists"], ref["d_dists"], **tol)
+    assert_close("d_target", got["d_target"], ref["d_target"], **tol)
+    dW = padded(ref["dW"], w.wp.shape)
+    assert_close("dB", got["dB"], padded(ref["db"], w.bp.shape), **tol)
+    worst_col = 0.0
+    for l, (k, n) in enumerate(x.shape for x in ws):
+        want = dW[l, :k, :n]
+        err = np.abs(got["dW"][l, :k, :n] - want)
+        cmax = np.abs(want).max(axis=0, keepdims=True)
+        lim = 1e-5 * np.abs(want) + F16X3_COL_TOL * cmax
+        assert (err <= lim).all(), (l, float((err / np.maximum(lim, 1e-300)).max()))
+        live = cmax[0] > 0
+        worst_col = max(worst_col, float((err.max(axis=0)[live] / cmax[0][live]).max(initial=0.0)))
+    worst = max((float(f.max()) for f in ref["flip_margins"] if len(f)), default=0.0)
+    assert worst <= FLIP_MARGIN
+    print(f"tiny-sigma batch: worst per-column dW error {worst_col:.3g} of the column max")

@@ -121,5 +121,17 @@ def test_int24_activation_slabs_move_12_bytes_per_lane(asm):
     assert k1 and k2
     for name, insts in k1.items():
         assert any(i.mn == "global_store_dwordx3" for i in insts), name
+        # the packed int24 data (v_perm_b32 results) leaves only through 12-B stores: a store
+        # widened to 16 B would overwrite the neighbouring lane's 4 bytes (the 12-B runs
+        # are only 4-B aligned), so no dwordx4 store may take a register v_perm_b32 wrote last
+        last = {}
+        for i in insts:
+            if i.mn.startswith("global_store"):
+                data = isa_check.regs_of(i.ops.split(",")[1]) if "," in i.ops else frozenset()
+                perm = {r for r in data if last.get(r) == "v_perm_b32"}
+                if perm:
+                    assert i.mn == "global_store_dwordx3", (name, hex(i.addr), i.mn, i.ops)
+            for r in getattr(i, "vdst", ()):
+                last[r] = i.mn
     for name, insts in k2.items():
         assert any(i.mn == "global_load_dwordx3" for i in insts), name

@@ -498,7 +498,9 @@ static void check_precision_flags(int flags) {
 extern "C" const char* lnerf_last_error(void) { return g_last_error.c_str(); }
 extern "C" const char* lnerf_version(void) { return "loma-nerf-amd 0.5 (gfx950)"; }
 
-extern "C" unsigned lnerf_build_knobs(void) { return lnerf::k16_build_knobs() | lnerf::dw16_build_knobs(); }
+extern "C" unsigned lnerf_build_knobs(void) {
+    return lnerf::k16_build_knobs() | lnerf::dw16_build_knobs() | lnerf::kr_build_knobs();
+}
 
 extern "C" int lnerf_ctx_create(lnerf_ctx** out, int device) {
     return guard_int([&]() {

@@ -21,6 +21,10 @@
 //  * partials per split, summed in order by grad_reduce_kernel (deterministic, no atomics).
 #include "lnerf_internal.h"
 
+#include <stddef.h>
+
+#include <algorithm>
+
 namespace lnerf {
 
 namespace {
@@ -40,6 +44,14 @@ typedef _Float16 hf4 __attribute__((ext_vector_type(4)));
 #ifndef LNERF_DW16_DEPTH
 #define LNERF_DW16_DEPTH 3
 #endif
+// ORDER 1: workgroups dispatched newest-slabs-first -- workgroup b takes the (layer, split) whose
+// sample range k1 wrote last (the tail of the batch: k1's last workgroup round), interleaving the
+// layers, so the first k2 workgroups read slabs still resident in the Infinity Cache; 0: layer by
+// layer, first samples first
+#ifndef LNERF_DW16_ORDER
+#define LNERF_DW16_ORDER 0
+#endif
+constexpr int kMaxMap = 1024;   // workgroups the ORDER map covers (the kernel-argument table)
 
 constexpr int kThreads = 512;
 constexpr int kRows = 512;                  // A rows [0, 256) and G rows [256, 512) of the image
@@ -77,6 +89,8 @@ struct Dw16Args {
     int rpad;                   // slab positions per layer
     const int* eshift;          // per-layer product shift E_l (k1_reduce_kernel)
     int L;
+    int use_map;                // ORDER: map[blockIdx] = layer << 12 | split
+    unsigned short map[kMaxMap];
 };
 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
@@ -547,9 +561,22 @@ __host__ __device__ __forceinline__ int dw_shape(int kt, int nt) {
 template <int PL>
 __global__ void __launch_bounds__(kThreads, 1) dw16_kernel(Dw16Args a) {
     __shared__ __attribute__((aligned(16))) unsigned char lds[2 * image_bytes<PL>()];
-    int li = 0;
-    while (li + 1 < a.nl && (int)blockIdx.x >= a.wg_off[li + 1]) ++li;
-    const int l = a.lid[li], sp = blockIdx.x - a.wg_off[li];
+    int l, sp;
+    if (a.use_map) {
+        // a scalar load from the kernel-argument segment (indexing the by-value table would copy it)
+        const __attribute__((address_space(4))) unsigned short* t =
+            (const __attribute__((address_space(4))) unsigned short*)((const __attribute__((address_space(4))) char*)
+                                                                          __builtin_amdgcn_kernarg_segment_ptr() +
+                                                                      offsetof(Dw16Args, map));
+        const int e = t[blockIdx.x];
+        l = e >> 12;
+        sp = e & 0xFFF;
+    } else {
+        int li = 0;
+        while (li + 1 < a.nl && (int)blockIdx.x >= a.wg_off[li + 1]) ++li;
+        l = a.lid[li];
+        sp = blockIdx.x - a.wg_off[li];
+    }
     switch (dw_shape(a.kt[l], a.nt[l])) {
         case 0: dw_split<PL, 1, 1>(a, l, sp, lds); break;
         case 1: dw_split<PL, 1, 2>(a, l, sp, lds); break;
@@ -604,7 +631,8 @@ __global__ void __launch_bounds__(1024) k1_reduce_kernel(const int* __restrict__
 // compile-time settings of this object that differ from the product build (lnerf_build_knobs)
 unsigned dw16_build_knobs() {
     return (LNERF_DW16_SPLIT_LATE != 1 ? kKnobDwSplitLate : 0u) | (LNERF_DW16_DEPTH != 3 ? kKnobDwDepth : 0u) |
-           (LNERF_DW16_SWZ != 1 ? kKnobDwSwz : 0u) | (LNERF_A24 != 1 ? kKnobA24 : 0u);
+           (LNERF_DW16_SWZ != 1 ? kKnobDwSwz : 0u) | (LNERF_A24 != 1 ? kKnobA24 : 0u) |
+           (LNERF_DW16_ORDER != 0 ? kKnobDwOrder : 0u);
 }
 
 void dw16_launch(const FusedPlan& p, hipStream_t s) {
@@ -631,6 +659,22 @@ void dw16_launch(const FusedPlan& p, hipStream_t s) {
     a.rpad = p.num_wg * p.tile;
     a.eshift = p.dw_shift;
     a.L = p.L;
+    if (LNERF_DW16_ORDER == 1 && p.dw_grid <= kMaxMap) {
+        // newest slabs first: key (sp + 1/2) / splits_l, descending (k1's workgroups run in blockIdx
+        // order, so the last sample ranges were written last), layers interleaved at equal keys
+        struct E {
+            double key;
+            int l, sp;
+        };
+        E e[kMaxMap];
+        int n = 0;
+        for (int l = 0; l < p.L; ++l)
+            for (int sp = 0; sp < p.dw_splits[l]; ++sp) e[n++] = E{(sp + 0.5) / p.dw_splits[l], l, sp};
+        std::stable_sort(e, e + n, [](const E& x, const E& y) { return x.key > y.key; });
+        for (int i = 0; i < n; ++i) a.map[i] = (unsigned short)(e[i].l << 12 | e[i].sp);
+        a.use_map = n == p.dw_grid ? 1 : 0;
+    }
+    static_assert(sizeof(Dw16Args) <= 4096, "kernel arguments");
     // the per-layer product shifts of k1_reduce_launch (launched right after k1)
     if (p.x6 == 2) dw16_kernel<2><<<p.dw_grid, kThreads, 0, s>>>(a);
     else if (p.x6 == 3) dw16_kernel<3><<<p.dw_grid, kThreads, 0, s>>>(a);

@@ -67,9 +67,11 @@ enum : unsigned {
     kKnobK16FullDma = 1u << 0, kKnobK16KDist = 1u << 1, kKnobK16SplitAt = 1u << 2, kKnobK16Sched = 1u << 3,
     kKnobK16Prio = 1u << 4, kKnobK16Spread = 1u << 5, kKnobProf = 1u << 6, kKnobA24 = 1u << 7,
     kKnobK16Only = 1u << 8, kKnobDwSplitLate = 1u << 9, kKnobDwDepth = 1u << 10, kKnobDwSwz = 1u << 11,
+    kKnobK16Pin = 1u << 12, kKnobK16FdSrc = 1u << 13, kKnobDwOrder = 1u << 14, kKnobKrStagger = 1u << 15,
 };
 unsigned k16_build_knobs();
 unsigned dw16_build_knobs();
+unsigned kr_build_knobs();
 
 // ---- ray sampling (train_nerf.py:289-306), float64 as numpy computes it -----------------------
 // t_j = np.linspace(near, far, S)[j]: j * ((far - near) / (S - 1)) + near, the last one = far.

@@ -276,22 +276,41 @@ __device__ __forceinline__ void store_slab_step(float* __restrict__ dst, const f
 // as y = x 2^(ex + 8) + 1.5 2^23 (round-to-nearest integer q in the mantissa field, |q| < 2^22;
 // ex = the sample's row shift), their low 24 bits packed 4 to 12 B by v_perm_b32, two
 // global_store_dwordx3 into the 1.5-KiB half-block run [feature half 2][16 samples][16 f] x 3 B.
-__device__ __forceinline__ void store_slab_step24(unsigned char* __restrict__ dst, const fx4& t0, const fx4& t1,
-                                                  int ex) {
-    // 4-byte aligned (the 12-B runs sit at 12 g): a plain 3-vector claims 16-B size and alignment,
-    // which would let the compiler widen the store over the neighbouring lane's bytes
-    typedef unsigned u3 __attribute__((ext_vector_type(3), aligned(4)));
-    const int lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
+typedef unsigned u3a __attribute__((ext_vector_type(3), aligned(4)));
+struct Packed24 {
+    u3a p0, p1;
+};
+// the 8 values as y = x 2^(ex + 8) + 1.5 2^23, low 24 bits of four y packed into 12 B (v_perm_b32)
+__device__ __forceinline__ Packed24 pack_slab_step24(const fx4& t0, const fx4& t1, int ex) {
     constexpr float kMagic = 12582912.0f;   // 1.5 2^23
     auto pack = [&](const fx4& t) {
         unsigned y[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) y[i] = __builtin_bit_cast(unsigned, __builtin_ldexpf(t[i], ex + 8) + kMagic);
-        return u3{__builtin_amdgcn_perm(y[1], y[0], 0x04020100u), __builtin_amdgcn_perm(y[2], y[1], 0x05040201u),
-                  __builtin_amdgcn_perm(y[3], y[2], 0x06050402u)};
+        return u3a{__builtin_amdgcn_perm(y[1], y[0], 0x04020100u), __builtin_amdgcn_perm(y[2], y[1], 0x05040201u),
+                   __builtin_amdgcn_perm(y[3], y[2], 0x06050402u)};
     };
-    __builtin_nontemporal_store(pack(t0), (u3*)(dst + n * 48 + 12 * g));
-    __builtin_nontemporal_store(pack(t1), (u3*)(dst + 768 + n * 48 + 12 * g));
+    return Packed24{pack(t0), pack(t1)};
+}
+// two global_store_dwordx3 into the 1.5-KiB half-block run [feature half 2][16 samples][16 f] x 3 B
+// (4-byte aligned: the 12-B runs sit at 12 g; a plain 3-vector claims 16-B size and alignment,
+// which would let the compiler widen the store over the neighbouring lane's bytes)
+__device__ __forceinline__ void store_packed24(unsigned char* __restrict__ dst, const Packed24& v) {
+    const int lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
+    __builtin_nontemporal_store(v.p0, (u3a*)(dst + n * 48 + 12 * g));
+    __builtin_nontemporal_store(v.p1, (u3a*)(dst + 768 + n * 48 + 12 * g));
+}
+__device__ __forceinline__ void store_slab_step24(unsigned char* __restrict__ dst, const fx4& t0, const fx4& t1,
+                                                  int ex) {
+    store_packed24(dst, pack_slab_step24(t0, t1, ex));
+}
+
+// Materialise a value here: an empty asm that reads and writes it in place (no instruction; the
+// compiler may not compute it later than this point, nor move this point across the
+// sched_barriers around it)
+template <typename T>
+__device__ __forceinline__ void pin(T& v) {
+    asm volatile("" : "+v"(v));
 }
 
 // A weight fragment: one ds_read_b128 per lane (the compiler counts it and places its wait).
@@ -329,6 +348,19 @@ __device__ __forceinline__ void read_tile(const unsigned char* base, bf8 (&w)[3]
 #ifndef LNERF_K16_SPREAD
 #define LNERF_K16_SPREAD 1
 #endif
+// PIN: the next k-step's operand split and this k-step's int24 slab packing are pinned between
+// the two halves of the output tiles (an empty asm that "reads and writes" their registers),
+// where the partner wave's MFMAs cover them; without it the compiler sinks both next to their
+// first use, at the k-step boundary, where both waves of a SIMD issue them together
+#ifndef LNERF_K16_PIN
+#define LNERF_K16_PIN 0
+#endif
+// FDSRC: a whole chunk of a full pass takes its source address from the pass base (an SGPR the
+// layer loop loads once) instead of the chunk table (a scalar load + lgkmcnt(0) per chunk, right
+// after the barrier)
+#ifndef LNERF_K16_FDSRC
+#define LNERF_K16_FDSRC 0
+#endif
 constexpr int kPiecesMax = 8;   // pieces per wave of a full chunk (64 KiB / 8 waves, 32 KiB / 4)
 struct DmaJob {
     const char* src = nullptr;   // the wave's (uniform) address of piece 0
@@ -350,9 +382,16 @@ __device__ __forceinline__ void dma_pieces_at(const DmaJob& j, std::integer_sequ
 // Output tile O of one k-step: issue the reads of tile O + kDist, the MFMAs of tile O (small
 // terms first; the compiler waits for tile O's reads only, lgkmcnt(N) with the younger ones in
 // flight).
-template <int NTO, int PL, int NW, bool FD, int O>
+// no VALU filler between the tiles (see FillSpread)
+struct NoFill {
+    template <int O>
+    __device__ __forceinline__ void at() {}
+};
+
+template <int NTO, int PL, int NW, bool FD, int O, typename F = NoFill>
 __device__ __forceinline__ void tile_step(const unsigned char* base, bf8 (&w)[kDist + 1][3], const bf8& bh,
-                                          const bf8& bm, const bf8& bl, fx4 (&out)[kMaxT], const DmaJob& job) {
+                                          const bf8& bm, const bf8& bl, fx4 (&out)[kMaxT], const DmaJob& job,
+                                          F& fill) {
     if constexpr (O + kDist < NTO) read_tile<PL, O + kDist>(base, w[(O + kDist) % (kDist + 1)]);
     if constexpr (FD) dma_pieces_at<NTO, O, NW, true>(job, std::make_integer_sequence<int, kPiecesMax>{});
     else if (job.n) dma_pieces_at<NTO, O, NW, false>(job, std::make_integer_sequence<int, kPiecesMax>{});
@@ -378,15 +417,56 @@ __device__ __forceinline__ void tile_step(const unsigned char* base, bf8 (&w)[kD
         acc = mfma16(c[0], bh, acc);
     }
     out[O] = acc;
+    fill.template at<O>();
 }
 
 // tiles B, B+1, ... of one k-step
-template <int NTO, int PL, int NW, bool FD, int B, int... O>
+template <int NTO, int PL, int NW, bool FD, int B, typename F, int... O>
 __device__ __forceinline__ void tile_steps(std::integer_sequence<int, O...>, const unsigned char* base,
                                            bf8 (&w)[kDist + 1][3], const bf8& bh, const bf8& bm,
-                                           const bf8& bl, fx4 (&out)[kMaxT], const DmaJob& job) {
-    (tile_step<NTO, PL, NW, FD, B + O>(base, w, bh, bm, bl, out, job), ...);
+                                           const bf8& bl, fx4 (&out)[kMaxT], const DmaJob& job, F& fill) {
+    (tile_step<NTO, PL, NW, FD, B + O>(base, w, bh, bm, bl, out, job, fill), ...);
 }
+
+// LNERF_K16_PIN = 2 (fp16x3, 16 output tiles): the next k-step's operand split and this k-step's
+// int24 packing as VALU fillers spread over the first 12 tiles, a few instructions after each
+// tile's MFMAs (pair q of the split after tile 2q + 1, the two 12-B packs after tiles 9 and 11),
+// each result pinned there (in place, no instruction) so the compiler cannot sink it back to the
+// k-step boundary
+struct FillSpread {
+    const fx4* in;        // the pass input (in[2 sn], in[2 sn + 1]: the next k-step's features)
+    int sn;               // the next k-step
+    bool split;           // there is a next k-step
+    float sc;             // 2^ex
+    unsigned hv[4], lv[4];
+    bool pack;            // this k-step's int24 slab values are packed (stored after the last tile)
+    int s, ex;
+    Packed24 pk;
+    template <int O>
+    __device__ __forceinline__ void at() {
+        if constexpr (O == 1 || O == 3 || O == 5 || O == 7) {
+            constexpr int q = (O - 1) / 2;
+            if (split) {
+                const fx4& t = in[2 * sn + (q >> 1)];
+                split_h2(t[2 * (q & 1)], t[2 * (q & 1) + 1], sc, hv[q], lv[q]);
+                pin(hv[q]);
+                pin(lv[q]);
+            }
+        }
+        if constexpr (O == 9 || O == 11) {
+            if (pack) {
+                const Packed24 p = pack_slab_step24(in[2 * s], in[2 * s + 1], ex);
+                if constexpr (O == 9) {
+                    pk.p0 = p.p0;
+                    pin(pk.p0);
+                } else {
+                    pk.p1 = p.p1;
+                    pin(pk.p1);
+                }
+            }
+        }
+    }
+};
 
 // The B operand planes of k-step s (the lane's 8 input features phi(s, g, 0..7) of its sample):
 // bf16x6 hi/mid/lo, fp16x3 hi/lo (x 2^ex), or plain bf16.
@@ -435,8 +515,9 @@ template <int NTO, int PL, int NW, bool FD = false, bool A24 = false>
 __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk, bool last, int& ci,
                                          unsigned char* ring, float* bias_ring, const fx4 (&in)[kMaxT],
                                          fx4 (&out)[kMaxT], float* __restrict__ slab, int ex, bf8& bh,
-                                         bf8& bm, bf8& bl, int& pending) {
+                                         bf8& bm, bf8& bl, int& pending, const unsigned short* fdsrc) {
     using R = Ring<PL, NW>;
+    constexpr int KC_BYTES = R::KC * NTO * PL * 1024;
     const int lane = threadIdx.x & 63;
     const unsigned char* base = ring + (ci % R::slots) * R::slot_bytes + kk * NTO * PL * 1024 + lane * 16;
     const bool st = slab != nullptr;
@@ -448,7 +529,8 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
         // now, before the first weight tiles; spread: one piece per kPiecesMax-th of the output
         // tiles, between the MFMAs. The barrier waits for this wave's pieces of chunk ci + 1 only:
         // the slab stores issued after them (two per k-step) stay in flight.
-        const ChunkT c = chunk_at(a, ci + 1);
+        // FDSRC: the next chunk of this full pass, whole, no biases (fdsrc = its source)
+        const ChunkT c = (FD && LNERF_K16_FDSRC) ? ChunkT{fdsrc, KC_BYTES, -1} : chunk_at(a, ci + 1);
         unsigned char* dst = ring + ((ci + 1) % R::slots) * R::slot_bytes;
         int issued;
         if constexpr (spread) {
@@ -477,20 +559,63 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
     if constexpr (NTO > 1) read_tile<PL, 1>(base, w[1]);
     if constexpr (NTO > 2 && kDist > 2) read_tile<PL, 2>(base, w[2]);
     static_assert(kDist == 2 || kDist == 3, "the prologue reads kDist tiles");
+    Packed24 pk{};
     auto store = [&]() {
-        if constexpr (A24) store_slab_step24((unsigned char*)slab + s * 3072, in[2 * s], in[2 * s + 1], ex);
-        else store_slab_step(slab + s * 1024, in[2 * s], in[2 * s + 1]);
+        if constexpr (A24) {
+            if constexpr (LNERF_K16_PIN == 1) store_packed24((unsigned char*)slab + s * 3072, pk);
+            else store_slab_step24((unsigned char*)slab + s * 3072, in[2 * s], in[2 * s + 1], ex);
+        } else {
+            store_slab_step(slab + s * 1024, in[2 * s], in[2 * s + 1]);
+        }
     };
     if (st && !spread) store();
     // first half of the output tiles, [late waves: barrier], the next k-step's operand split (off
     // the next prologue's critical path), second half, [spread: the slab stores, younger than
     // every piece], [early: barrier]
     constexpr int H = NTO >= 4 ? NTO * LNERF_K16_SPLIT_AT / 4 : (NTO + 1) / 2;   // split after tile H
-    tile_steps<NTO, PL, NW, FD, 0>(std::make_integer_sequence<int, H>{}, base, w, bh, bm, bl, out, job);
+    constexpr bool spread_fill = LNERF_K16_PIN == 2 && PL == 2 && NTO == 16 && !R::stagger;
+    if constexpr (spread_fill) {
+        FillSpread f;
+        f.in = in;
+        f.sn = s + 1 < 8 ? s + 1 : 0;
+        f.split = s + 1 < ks;
+        f.sc = __builtin_ldexpf(1.0f, ex);
+        f.pack = A24 && st && spread;
+        f.s = s;
+        f.ex = ex;
+        tile_steps<NTO, PL, NW, FD, 0>(std::make_integer_sequence<int, NTO>{}, base, w, bh, bm, bl, out, job, f);
+        if (st && spread) {
+            asm volatile("" ::: "memory");
+            if constexpr (A24) store_packed24((unsigned char*)slab + s * 3072, f.pk);
+            else store_slab_step(slab + s * 1024, in[2 * s], in[2 * s + 1]);
+        }
+        if (!late && last) dma_barrier(pending);
+        if (last) ++ci;
+        typedef unsigned u4 __attribute__((ext_vector_type(4)));
+        bh = f.split ? __builtin_bit_cast(bf8, u4{f.hv[0], f.hv[1], f.hv[2], f.hv[3]}) : bf8{};
+        bm = f.split ? __builtin_bit_cast(bf8, u4{f.lv[0], f.lv[1], f.lv[2], f.lv[3]}) : bf8{};
+        return;
+    }
+    NoFill nf;
+    tile_steps<NTO, PL, NW, FD, 0>(std::make_integer_sequence<int, H>{}, base, w, bh, bm, bl, out, job, nf);
     if (late && last) dma_barrier(pending);
     bf8 nh = {}, nm = {}, nl = {};
     if (s + 1 < ks) make_b<PL>(in, s + 1 < 8 ? s + 1 : 0, ex, nh, nm, nl);
-    tile_steps<NTO, PL, NW, FD, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, bh, bm, bl, out, job);
+    if constexpr (LNERF_K16_PIN == 1) {
+        if (s + 1 < ks) {
+            pin(nh);
+            if constexpr (PL >= 2) pin(nm);
+            if constexpr (PL == 3) pin(nl);
+        }
+        if constexpr (A24) {
+            if (st && spread) {
+                pk = pack_slab_step24(in[2 * s], in[2 * s + 1], ex);
+                pin(pk.p0);
+                pin(pk.p1);
+            }
+        }
+    }
+    tile_steps<NTO, PL, NW, FD, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, bh, bm, bl, out, job, nf);
     if (st && spread) {
         asm volatile("" ::: "memory");
         store();
@@ -509,45 +634,49 @@ template <int NTO, int PL, int NW, bool FULL, bool A24, int S>
 __device__ __forceinline__ void k16_pass_step(const K16Args& a, int ks, int& ci, unsigned char* ring,
                                               float* bias_ring, const fx4 (&in)[kMaxT], fx4 (&out)[kMaxT],
                                               float* __restrict__ slab, int ex, bf8& bh, bf8& bm, bf8& bl,
-                                              int& pending) {
+                                              int& pending, const unsigned short* pbase) {
     constexpr int KC = Ring<PL, NW>::KC;
     if (FULL || S < ks) {
         constexpr int kk = S % KC;
         const bool last = kk == KC - 1 || (FULL ? S == 7 : S + 1 == ks);
         constexpr bool fd = LNERF_K16_FULLDMA && FULL && kk == 0 && S / KC + 1 < 8 / KC &&
                             KC * NTO * PL == kPiecesMax * NW && LNERF_K16_SPREAD && !Ring<PL, NW>::stagger;
+        // the source of the chunk after this one (S / KC + 1 of the pass), for FDSRC
+        const unsigned short* fdsrc = pbase + (size_t)(S / KC + 1) * (KC * NTO * PL * 512);
         k16_step<NTO, PL, NW, fd, A24>(a, FULL ? 8 : ks, S, kk, last, ci, ring, bias_ring, in, out, slab, ex, bh,
-                                       bm, bl, pending);
+                                       bm, bl, pending, fdsrc);
     }
 }
 template <int NTO, int PL, int NW, bool FULL, bool A24, int... S>
 __device__ __forceinline__ void k16_pass_steps(std::integer_sequence<int, S...>, const K16Args& a, int ks, int& ci,
                                                unsigned char* ring, float* bias_ring, const fx4 (&in)[kMaxT],
                                                fx4 (&out)[kMaxT], float* __restrict__ slab, int ex, bf8& bh,
-                                               bf8& bm, bf8& bl, int& pending) {
-    (k16_pass_step<NTO, PL, NW, FULL, A24, S>(a, ks, ci, ring, bias_ring, in, out, slab, ex, bh, bm, bl, pending), ...);
+                                               bf8& bm, bf8& bl, int& pending, const unsigned short* pbase) {
+    (k16_pass_step<NTO, PL, NW, FULL, A24, S>(a, ks, ci, ring, bias_ring, in, out, slab, ex, bh, bm, bl, pending,
+                                              pbase), ...);
 }
 
 // One pass (a layer's forward or backward MMA) over its ks k-steps, Ring::KC k-steps per chunk.
 // A24: the pass's input slab (a forward pass's A_{l-1}) is int24 (store_slab_step24).
+// pbase: the pass's first chunk in w16 (FULL passes with FDSRC; otherwise unused)
 template <int NTO, int PL, int NW, bool FULL = false, bool A24 = false>
 __device__ __forceinline__ void k16_pass(const K16Args& a, int ks, int& ci, unsigned char* ring,
                                          float* bias_ring, const fx4 (&in)[kMaxT], fx4 (&out)[kMaxT],
-                                         float* __restrict__ slab, int ex = 0) {
+                                         float* __restrict__ slab, int ex = 0, const unsigned short* pbase = nullptr) {
     bf8 bh = {}, bm = {}, bl = {};
     make_b<PL>(in, 0, ex, bh, bm, bl);
     int pending = 0;
     k16_pass_steps<NTO, PL, NW, FULL, A24>(std::make_integer_sequence<int, 8>{}, a, ks, ci, ring, bias_ring, in, out,
-                                           slab, ex, bh, bm, bl, pending);
+                                           slab, ex, bh, bm, bl, pending, pbase);
 }
 // a hidden layer's pass: the FULL instantiation for 256-wide inputs (every hidden layer of cfg3)
 template <int HT, int PL, int NW, bool A24 = false>
 __device__ __forceinline__ void k16_hidden_pass(const K16Args& a, int ks, int& ci, unsigned char* ring,
                                                 float* bias_ring, const fx4 (&in)[kMaxT], fx4 (&out)[kMaxT],
-                                                float* __restrict__ slab, int ex) {
+                                                float* __restrict__ slab, int ex, const unsigned short* pbase) {
     if constexpr (LNERF_K16_FULLDMA && HT == 16) {
         if (ks == 8) {
-            k16_pass<HT, PL, NW, true, A24>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
+            k16_pass<HT, PL, NW, true, A24>(a, ks, ci, ring, bias_ring, in, out, slab, ex, pbase);
             return;
         }
     }
@@ -773,7 +902,8 @@ k16_fwd_bwd_kernel(K16Args a) {
         const int sh = unscale(l, ex);
         if (l < a.L - 1) {
             PROF_T(t_f);
-            k16_hidden_pass<HT, PL, NW, a24_slabs(PL)>(a, a.ks_f[l], ci, ring, bias_ring, act, out, slab, ex);
+            k16_hidden_pass<HT, PL, NW, a24_slabs(PL)>(a, a.ks_f[l], ci, ring, bias_ring, act, out, slab, ex,
+                                                       a.w16 + a.wf_off[l]);
             PROF_ADD(kPfFwd, t_f);
             PROF_T(t_fe);
             // bias after the sum (nerf.py:98,125), ReLU (nerf.py:141-144) and its mask bits
@@ -835,7 +965,7 @@ k16_fwd_bwd_kernel(K16Args a) {
         store_emin(a, l, exa.get(l), store_sexp(a, l, 1, xm));
         const int ex = shift_of(xm);
         const int sh = unscale(l, ex);
-        k16_hidden_pass<HT, PL, NW>(a, a.ks_b[l], ci, ring, bias_ring, act, out, slab, ex);
+        k16_hidden_pass<HT, PL, NW>(a, a.ks_b[l], ci, ring, bias_ring, act, out, slab, ex, a.w16 + a.wb_off[l]);
         PROF_ADD(kPfBwd, t_b);
         PROF_T(t_be);
         // the forward's decision as an all-ones / zero lane mask (v_bfe_i32), one AND per value
@@ -1002,7 +1132,8 @@ unsigned k16_build_knobs() {
     return (LNERF_K16_FULLDMA != 1 ? kKnobK16FullDma : 0u) | (LNERF_K16_KDIST != 2 ? kKnobK16KDist : 0u) |
            (LNERF_K16_SPLIT_AT != 2 ? kKnobK16SplitAt : 0u) | (LNERF_K16_SCHED != 1 ? kKnobK16Sched : 0u) |
            (LNERF_K16_PRIO != 0 ? kKnobK16Prio : 0u) | (LNERF_K16_SPREAD != 1 ? kKnobK16Spread : 0u) |
-           (LNERF_PROF != 0 ? kKnobProf : 0u) | (LNERF_A24 != 1 ? kKnobA24 : 0u)
+           (LNERF_PROF != 0 ? kKnobProf : 0u) | (LNERF_A24 != 1 ? kKnobA24 : 0u) |
+           (LNERF_K16_PIN != 0 ? kKnobK16Pin : 0u) | (LNERF_K16_FDSRC != 0 ? kKnobK16FdSrc : 0u)
 #ifdef LNERF_K16_ONLY_16_2
            | kKnobK16Only
 #endif

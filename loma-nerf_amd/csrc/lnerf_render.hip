@@ -39,7 +39,16 @@ constexpr int kMaxT = 16;                        // 16-wide output tiles of a 25
 constexpr int kKC = 2;                           // k-steps per chunk
 constexpr int kSlot = kKC * kMaxT * 1024;        // one chunk: 2 k-steps x 16 tiles x 1 KiB
 constexpr int kMaxChunks = kMaxLayers * 4 + 1;   // <= 4 chunks per forward pass + the end marker
-constexpr int kOffComp = 2 * kSlot;              // ring: 2 slots
+// STAGGER: waves 4-7 (each the SIMD partner of wave w - 4) meet each chunk's barrier half a k-step
+// later than waves 0-3 (in the middle of the chunk's last k-step), so the two waves of a SIMD run
+// their chunk prologues and layer epilogues (bias + ReLU + bf16 conversion of 128 values) beside
+// the partner's MFMAs instead of in lockstep with them (MI355X_MICROARCH.md, two waves per SIMD,
+// item 9). The late waves still read chunk c - 1 while chunk c + 1 lands: three ring slots.
+#ifndef LNERF_KR_STAGGER
+#define LNERF_KR_STAGGER 0
+#endif
+constexpr int kSlots = LNERF_KR_STAGGER ? 3 : 2;
+constexpr int kOffComp = kSlots * kSlot;         // the ring
 constexpr int kOffRay = kOffComp + comp::kCompFloats * kTile * 4;
 constexpr int kOffBias = kOffRay + kTile * 4;
 constexpr int kLds = kOffBias + 3 * 256 * 4;     // + a 3-slot ring of layer biases
@@ -119,7 +128,7 @@ __device__ __forceinline__ Job chunk_job(const KrArgs& a, int ci, unsigned char*
     const int woff = wave * 1024;
     j.n = (c.src && woff < c.bytes) ? (c.bytes - woff + kWaves * 1024 - 1) / (kWaves * 1024) : 0;
     j.src = c.src + woff + lane * 16;
-    j.dst = ring + (ci & 1) * kSlot + woff;
+    j.dst = ring + (ci % kSlots) * kSlot + woff;
     if (c.bias >= 0 && wave == kWaves - 1)
         glds16(a.b16 + (size_t)c.bias * 256 + lane * 4, lds_addr(bias_ring + (c.bias % 3) * 256));
     return j;
@@ -171,6 +180,13 @@ __device__ __forceinline__ void kr_tiles(std::integer_sequence<int, O...>, const
                                          fx4 (&acc)[kGroups][kMaxT], const Job& job) {
     (kr_tile<NTO, O>(base, w, b0, b1, acc, job), ...);
 }
+// tiles B, B + 1, ... of one k-step
+template <int NTO, int B, int... O>
+__device__ __forceinline__ void kr_tiles_from(std::integer_sequence<int, O...>, const unsigned char* base,
+                                              bf8 (&w)[kDist + 1], const bf8& b0, const bf8& b1,
+                                              fx4 (&acc)[kGroups][kMaxT], const Job& job) {
+    (kr_tile<NTO, B + O>(base, w, b0, b1, acc, job), ...);
+}
 
 // k-step S of a pass (S < ks): chunk ci's sub-step S % 2; the first sub-step issues chunk ci + 1's
 // DMA, the last meets the barrier that waits for it.
@@ -183,10 +199,21 @@ __device__ __forceinline__ void kr_step(const KrArgs& a, int ks, int& ci, unsign
     Job job;
     if (kk == 0) job = chunk_job(a, ci + 1, ring, bias_ring);
     const int lane = threadIdx.x & 63;
-    const unsigned char* base = ring + (ci & 1) * kSlot + kk * NTO * 1024 + lane * 16;
+    const unsigned char* base = ring + (ci % kSlots) * kSlot + kk * NTO * 1024 + lane * 16;
     bf8 w[kDist + 1];
     w[0] = *(const bf8*)(base);
     if constexpr (NTO > 1) w[1] = *(const bf8*)(base + 1024);
+    if constexpr (LNERF_KR_STAGGER) {
+        // late waves: the barrier after the first half of the last k-step's tiles
+        constexpr int H = NTO / 2;
+        const bool late = wave_id() >= 4;
+        kr_tiles_from<NTO, 0>(std::make_integer_sequence<int, H>{}, base, w, B[0][S], B[1][S], acc, job);
+        if (last && late) chunk_barrier();
+        kr_tiles_from<NTO, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, B[0][S], B[1][S], acc, job);
+        if (last && !late) chunk_barrier();
+        if (last) ++ci;
+        return;
+    }
     kr_tiles<NTO>(std::make_integer_sequence<int, NTO>{}, base, w, B[0][S], B[1][S], acc, job);
     if (last) {
         chunk_barrier();
@@ -339,6 +366,9 @@ kr_fwd_kernel(KrArgs a) {
 
 // plain bf16, the NeRF head, whole rays of <= 128 samples, a layer-0 input of <= 64 features
 // (PE with F <= 10); anything else renders on k16's forward
+// compile-time settings of this object that differ from the product build (lnerf_build_knobs)
+unsigned kr_build_knobs() { return LNERF_KR_STAGGER != 0 ? kKnobKrStagger : 0u; }
+
 bool kr_supported(const FusedPlan& p) {
     return p.x6 == 1 && !p.head_fit && p.S <= 128 && p.n[p.L - 1] <= 16 && p.tile == 128 && p.k[0] <= 64;
 }

@@ -226,7 +226,8 @@ static size_t workspace_floats(const lnerf_mlp& m, int rays, int S, bool train, 
     return align_up(y.act_total, 64) + align_up(y.grad_total, 64) + align_up((size_t)y.num_wg, 64) +
            align_up(y.dwp_total, 64) + align_up(y.dbp_total, 64) + 64 + align_up((y.w16_total + 1) / 2, 64) +
            align_up(y.b16_total, 64) + align_up(y.mask_total * 2, 64) + 64 +   // + the fp16x3 shifts
-           align_up((size_t)kMaxLayers * kWmaxParts, 64) +                       // per-block max|W|
+           align_up((size_t)kMaxLayers * kWmaxParts + kWmaxParts * kHeadCols, 64) +   // per-block max|W|
+           align_up((size_t)kHeadCols, 64) +                                     // head column max|W|
            (train ? align_up((size_t)m.num_layers * y.num_wg * tile / 2, 64) +   // per-sample shifts
                         align_up((size_t)m.num_layers * y.num_wg * 8, 64) : 0);     // per-wave minima
 }
@@ -299,7 +300,8 @@ static void fused_plan_tile(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch&
     p.mask_g = (unsigned long long*)take(y.mask_total * 2);
     p.wexp16 = (int*)take(2 * kMaxLayers);
     p.dw_shift = p.wexp16 + kMaxLayers;
-    p.wmax_part = (int*)take((size_t)kMaxLayers * kWmaxParts);
+    p.wmax_part = (int*)take((size_t)kMaxLayers * kWmaxParts + kWmaxParts * kHeadCols);
+    p.hexp16 = (int*)take((size_t)kHeadCols);
     p.sexp = (signed char*)(base + off);                             // L x num_wg x tile x 2 bytes
     if (train) off += align_up((size_t)p.L * y.num_wg * tile / 2, 64);
     p.epart = (int*)(base + off);

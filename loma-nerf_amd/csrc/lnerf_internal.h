@@ -11,6 +11,7 @@
 namespace lnerf {
 
 constexpr int kWmaxParts = 32;   // blocks per layer of the max|W| pass before the fp16x3 packing
+constexpr int kHeadCols = 16;    // head columns with their own fp16x3 weight shift (k16 head outputs)
 constexpr int kDefaultDwGrid = 512;   // dW workgroups per step unless LNERF_OPT_DW_GRID says otherwise
 
 // ---- fp16x3 exponent shifts ------------------------------------------------------------------
@@ -68,6 +69,7 @@ enum : unsigned {
     kKnobK16Prio = 1u << 4, kKnobK16Spread = 1u << 5, kKnobProf = 1u << 6, kKnobA24 = 1u << 7,
     kKnobK16Only = 1u << 8, kKnobDwSplitLate = 1u << 9, kKnobDwDepth = 1u << 10, kKnobDwSwz = 1u << 11,
     kKnobK16Pin = 1u << 12, kKnobK16FdSrc = 1u << 13, kKnobDwOrder = 1u << 14, kKnobKrStagger = 1u << 15,
+    kKnobK16Stag2 = 1u << 16,
 };
 unsigned k16_build_knobs();
 unsigned dw16_build_knobs();
@@ -198,7 +200,9 @@ struct FusedPlan {
     float* b16;                          // [L][256] zero-padded biases
     unsigned long long* mask_g;          // [num_wg][L-1][waves][64 lanes] ReLU mask bits
     int* wexp16;                         // x6 = 2: per-layer max|W| bits (fp16 weight plane shifts)
-    int* wmax_part;                      // x6 = 2: max|W| bits per layer and wmax block [L][kWmaxParts]
+    int* wmax_part;                      // x6 = 2: max|W| bits per layer and wmax block [L][kWmaxParts],
+                                         // then the head's per-column partials [kWmaxParts][kHeadCols]
+    int* hexp16;                         // x6 = 2: the head's per-column max|W| bits [kHeadCols]
     int* dw_shift;                       // per-layer dW product shift E_l (k1_reduce_kernel)
     signed char* sexp;                   // k1's per-sample slab shifts [L][num_wg * tile][2]
     int* epart;                          // k1's per-wave min of exA + exG [L][num_wg * waves]

@@ -43,6 +43,10 @@ constexpr int kWaves = 8;                     // the most waves per workgroup
 constexpr int kMaxChunks = 2 * kMaxLayers * 8 + 1;   // <= 2 passes x 8 k-steps per layer + 1 end
 constexpr int kMaxT = 16;                     // 16-feature tiles per 256-wide layer
 constexpr int kCompBytes = 2688 * 4;          // composite_tile's scratch (comp[0, 2688))
+// staggered wave pairs for fp16x3 on the 2-slot ring (Ring::stag2)
+#ifndef LNERF_K16_STAG2
+#define LNERF_K16_STAG2 0
+#endif
 // full hidden passes get compile-time step bounds and test-free DMA issue (A/B: 0 = generic only)
 #ifndef LNERF_K16_FULLDMA
 #define LNERF_K16_FULLDMA 1
@@ -62,8 +66,14 @@ constexpr int kCompBytes = 2688 * 4;          // composite_tile's scratch (comp[
 template <int PL, int NW = 8>
 struct Ring {
     static constexpr int KC = (PL == 3 || NW == 4) ? 1 : 2;
-    static constexpr bool stagger = PL == 3 && NW == 8;
-    static constexpr int slots = stagger ? 3 : 2;
+    // STAG2 (fp16x3, 8 waves): staggered wave pairs on the 2-slot ring of 2-k-step chunks. Waves 4-7
+    // meet each chunk's barrier after half of its last k-step's tiles, so they still read the tail of
+    // chunk c - 1 while chunk c + 1 lands in its slot: the early waves (0-3) DMA only the leading
+    // pieces of chunk c + 1 that the late waves have read already (ChunkT::early, from the chunk
+    // table), the late waves the rest once they are past chunk c - 1 (LNERF_K16_STAG2)
+    static constexpr bool stag2 = LNERF_K16_STAG2 && PL == 2 && NW == 8;
+    static constexpr bool stagger = (PL == 3 && NW == 8) || stag2;
+    static constexpr int slots = (PL == 3 && NW == 8) ? 3 : 2;
     static constexpr int slot_bytes = KC * kMaxT * PL * 1024;
     static constexpr int off_comp = slots * slot_bytes;
     static constexpr int off_ray = off_comp + kCompBytes;
@@ -105,6 +115,7 @@ struct K16Args {
     int want_grad;
     int planes;
     const int* wexp;   // PL = 2: per-layer max|W| bits of the packed fp16 weight planes (wshift_of)
+    const int* hexp;   // PL = 2: the head's per-column max|W| bits (head_col_shift)
     // training: every sample's exponent shift of each slab row (store_sexp), [l][position][2] int8:
     // byte 0 the input of layer l (X, A_l-1), byte 1 G_l; position = half-block * 16 + sample
     signed char* sexp;
@@ -167,6 +178,7 @@ struct ChunkT {
     const unsigned short* src;   // nullptr: past the last chunk
     int bytes;
     int bias;                    // layer whose biases ride with this chunk, -1: none
+    int early;                   // STAG2: leading 1-KiB pieces the early waves may DMA (k16_launch)
 };
 
 __device__ __forceinline__ ChunkT chunk_at(const K16Args& a, int ci) {
@@ -176,7 +188,7 @@ __device__ __forceinline__ ChunkT chunk_at(const K16Args& a, int ci) {
                                                             offsetof(K16Args, chunk_tab)) + 2 * ci;
     const unsigned off = t[0], e = t[1];
     const int bytes = (int)(e & 0xFFFFu) * 1024;
-    return ChunkT{bytes ? a.w16 + off : nullptr, bytes, (int)(e >> 16) - 1};
+    return ChunkT{bytes ? a.w16 + off : nullptr, bytes, (int)((e >> 16) & 0xFFu) - 1, (int)(e >> 24)};
 }
 
 // LDS-DMA (global_load_lds_dwordx4) of a chunk into its ring slot: 8 KiB per round of the
@@ -252,6 +264,14 @@ __device__ __forceinline__ void split_h(float xs, _Float16& h, _Float16& l) {
 // the exponent shift ew of a layer from its max|W| bits (fp16x3_shift) -- the weight-side half
 // of the fp16x3 scaling
 __device__ __forceinline__ int wshift_of(int maxbits) { return fp16x3_shift(__int_as_float(maxbits)); }
+
+// The head's per-column weight shift (planes = 2): column n of the head's packed planes is scaled by
+// 2^head_col_shift(n) -- its own max|W[:, n]| in [2^13, 2^14) -- instead of the layer's shift, so a
+// column far below the others (a sigma output whose weights are 2^-20 or 2^-30 of the rgb ones)
+// keeps fp16's normal range. An all-zero column keeps the layer's shift.
+__device__ __forceinline__ int head_col_shift(int colmax_bits, int layer_bits) {
+    return colmax_bits > 0 ? wshift_of(colmax_bits) : wshift_of(layer_bits);
+}
 
 
 // x = hi + mid + lo (round-to-nearest bf16 of each remainder; every remainder is exact in f32)
@@ -367,21 +387,31 @@ struct DmaJob {
     unsigned char* dst = nullptr;   // LDS address of this wave's piece 0
     int n = 0;                   // this wave's pieces of the chunk
 };
-template <int NW>
+// piece p of a job: STRIDE KiB apart (NW for the round-robin assignment; 4 for STAG2's, where the
+// four early or the four late waves share a chunk)
+template <int STRIDE>
 __device__ __forceinline__ void dma_piece(const DmaJob& j, int p) {
     const int lane = threadIdx.x & 63;
-    glds16(j.src + p * (NW * 1024) + lane * 16, lds_addr(j.dst + p * (NW * 1024)));
+    glds16(j.src + p * (STRIDE * 1024) + lane * 16, lds_addr(j.dst + p * (STRIDE * 1024)));
 }
-// the pieces that land on output tile O: p with p * NTO / kPiecesMax == O (all on tile 0 when NTO == 1);
-// FULL: the chunk is known to be whole (every wave issues kPiecesMax pieces, no per-piece test)
-template <int NTO, int O, int NW, bool FULL, int... P>
+// the pieces that land on output tile O: p with p * NTO / NP == O (all on tile 0 when NTO == 1);
+// FULL: the chunk is known to be whole (every wave issues NP pieces, no per-piece test)
+template <int NTO, int O, int STRIDE, bool FULL, int NP, int... P>
 __device__ __forceinline__ void dma_pieces_at(const DmaJob& j, std::integer_sequence<int, P...>) {
-    (((P * NTO) / kPiecesMax == O ? ((FULL || P < j.n) ? dma_piece<NW>(j, P) : void()) : void()), ...);
+    (((P * NTO) / NP == O ? ((FULL || P < j.n) ? dma_piece<STRIDE>(j, P) : void()) : void()), ...);
 }
+constexpr int kPiecesStag = 16;   // STAG2: at most 13 pieces per wave, one per output tile
 
 // Output tile O of one k-step: issue the reads of tile O + kDist, the MFMAs of tile O (small
 // terms first; the compiler waits for tile O's reads only, lgkmcnt(N) with the younger ones in
 // flight).
+// The output tile after which a k-step splits its next operands (and a late wave of a staggered
+// pair meets the chunk barrier)
+template <int NTO>
+constexpr int half_tiles() {
+    return NTO >= 4 ? NTO * LNERF_K16_SPLIT_AT / 4 : (NTO + 1) / 2;
+}
+
 // no VALU filler between the tiles (see FillSpread)
 struct NoFill {
     template <int O>
@@ -393,8 +423,17 @@ __device__ __forceinline__ void tile_step(const unsigned char* base, bf8 (&w)[kD
                                           const bf8& bm, const bf8& bl, fx4 (&out)[kMaxT], const DmaJob& job,
                                           F& fill) {
     if constexpr (O + kDist < NTO) read_tile<PL, O + kDist>(base, w[(O + kDist) % (kDist + 1)]);
-    if constexpr (FD) dma_pieces_at<NTO, O, NW, true>(job, std::make_integer_sequence<int, kPiecesMax>{});
-    else if (job.n) dma_pieces_at<NTO, O, NW, false>(job, std::make_integer_sequence<int, kPiecesMax>{});
+    if constexpr (Ring<PL, NW>::stag2) {
+        // over the first half_tiles only: a late wave of a one-k-step chunk meets the barrier there,
+        // and every piece must be older than its vmcnt
+        constexpr int HT2 = half_tiles<NTO>() < 1 ? 1 : half_tiles<NTO>();
+        if constexpr (O < HT2)
+            if (job.n) dma_pieces_at<HT2, O, 4, false, kPiecesStag>(job, std::make_integer_sequence<int, kPiecesStag>{});
+    } else if constexpr (FD) {
+        dma_pieces_at<NTO, O, NW, true, kPiecesMax>(job, std::make_integer_sequence<int, kPiecesMax>{});
+    } else if (job.n) {
+        dma_pieces_at<NTO, O, NW, false, kPiecesMax>(job, std::make_integer_sequence<int, kPiecesMax>{});
+    }
     // keep tile O + kDist's reads ahead of tile O's MFMAs: the machine scheduler otherwise sinks
     // each read next to its first consumer (one MFMA of slack, an LDS round trip exposed per tile);
     // the compiler still places every wait itself
@@ -521,7 +560,7 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
     const int lane = threadIdx.x & 63;
     const unsigned char* base = ring + (ci % R::slots) * R::slot_bytes + kk * NTO * PL * 1024 + lane * 16;
     const bool st = slab != nullptr;
-    constexpr bool spread = LNERF_K16_SPREAD && !R::stagger;
+    constexpr bool spread = LNERF_K16_SPREAD && (!R::stagger || R::stag2);
     DmaJob job;
     if (kk == 0) {
         // DMA of chunk ci + 1 (its table entry is a scalar load the compiler waits for with
@@ -529,11 +568,31 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
         // now, before the first weight tiles; spread: one piece per kPiecesMax-th of the output
         // tiles, between the MFMAs. The barrier waits for this wave's pieces of chunk ci + 1 only:
         // the slab stores issued after them (two per k-step) stay in flight.
-        // FDSRC: the next chunk of this full pass, whole, no biases (fdsrc = its source)
-        const ChunkT c = (FD && LNERF_K16_FDSRC) ? ChunkT{fdsrc, KC_BYTES, -1} : chunk_at(a, ci + 1);
+        // FDSRC: the next chunk of this full pass, whole, no biases (fdsrc = its source); under STAG2
+        // only from the pass's second chunk on (the slot's previous chunk is then this pass's, so the
+        // early waves' share is kStag2Early; the first chunk's predecessor is the previous pass's)
+        constexpr int kStag2H = half_tiles<NTO>();
+        constexpr int kStag2Early = (R::KC - 1) * NTO * PL + (NTO < kStag2H + kDist ? NTO : kStag2H + kDist) * PL;
+        const bool fdtab = FD && LNERF_K16_FDSRC && (!R::stag2 || s >= R::KC);
+        const ChunkT c = fdtab ? ChunkT{fdsrc, KC_BYTES, -1, kStag2Early} : chunk_at(a, ci + 1);
         unsigned char* dst = ring + ((ci + 1) % R::slots) * R::slot_bytes;
         int issued;
-        if constexpr (spread) {
+        if constexpr (R::stag2) {
+            // early waves: pieces e, e + 4, ... below c.early; late waves: the same residues above it
+            const int wave = wave_id(), e4 = wave & 3;
+            const int np = c.src ? c.bytes / 1024 : 0;
+            const int E = c.early < np ? c.early : np;
+            const int q0 = wave < 4 ? e4 : E + ((e4 - E) & 3);
+            const int q1 = wave < 4 ? E : np;
+            job.n = q0 < q1 ? (q1 - q0 + 3) / 4 : 0;
+            job.src = (const char*)c.src + q0 * 1024;
+            job.dst = dst + q0 * 1024;
+            issued = job.n;
+            if (c.bias >= 0 && wave == NW - 1) {
+                glds16(a.b16 + (size_t)c.bias * 256 + lane * 4, lds_addr(bias_ring + (c.bias % 3) * 256));
+                ++issued;
+            }
+        } else if constexpr (spread) {
             const int wave = wave_id();
             const int woff = wave * 1024;
             job.n = FD ? kPiecesMax
@@ -572,8 +631,10 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
     // first half of the output tiles, [late waves: barrier], the next k-step's operand split (off
     // the next prologue's critical path), second half, [spread: the slab stores, younger than
     // every piece], [early: barrier]
-    constexpr int H = NTO >= 4 ? NTO * LNERF_K16_SPLIT_AT / 4 : (NTO + 1) / 2;   // split after tile H
-    constexpr bool spread_fill = LNERF_K16_PIN == 2 && PL == 2 && NTO == 16 && !R::stagger;
+    constexpr int H = half_tiles<NTO>();   // split after tile H
+    constexpr bool spread_fill = LNERF_K16_PIN == 2 && PL == 2 && NTO == 16 && (!R::stagger || R::stag2);
+    // a late wave meets the barrier before this k-step's spread slab stores: they are not pending yet
+    const int late_pending = (st && spread && pending >= 2) ? pending - 2 : pending;
     if constexpr (spread_fill) {
         FillSpread f;
         f.in = in;
@@ -583,7 +644,9 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
         f.pack = A24 && st && spread;
         f.s = s;
         f.ex = ex;
-        tile_steps<NTO, PL, NW, FD, 0>(std::make_integer_sequence<int, NTO>{}, base, w, bh, bm, bl, out, job, f);
+        tile_steps<NTO, PL, NW, FD, 0>(std::make_integer_sequence<int, H>{}, base, w, bh, bm, bl, out, job, f);
+        if (late && last) dma_barrier(late_pending);
+        tile_steps<NTO, PL, NW, FD, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, bh, bm, bl, out, job, f);
         if (st && spread) {
             asm volatile("" ::: "memory");
             if constexpr (A24) store_packed24((unsigned char*)slab + s * 3072, f.pk);
@@ -598,7 +661,7 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
     }
     NoFill nf;
     tile_steps<NTO, PL, NW, FD, 0>(std::make_integer_sequence<int, H>{}, base, w, bh, bm, bl, out, job, nf);
-    if (late && last) dma_barrier(pending);
+    if (late && last) dma_barrier(late_pending);
     bf8 nh = {}, nm = {}, nl = {};
     if (s + 1 < ks) make_b<PL>(in, s + 1 < 8 ? s + 1 : 0, ex, nh, nm, nl);
     if constexpr (LNERF_K16_PIN == 1) {
@@ -640,7 +703,8 @@ __device__ __forceinline__ void k16_pass_step(const K16Args& a, int ks, int& ci,
         constexpr int kk = S % KC;
         const bool last = kk == KC - 1 || (FULL ? S == 7 : S + 1 == ks);
         constexpr bool fd = LNERF_K16_FULLDMA && FULL && kk == 0 && S / KC + 1 < 8 / KC &&
-                            KC * NTO * PL == kPiecesMax * NW && LNERF_K16_SPREAD && !Ring<PL, NW>::stagger;
+                            KC * NTO * PL == kPiecesMax * NW && LNERF_K16_SPREAD &&
+                            (!Ring<PL, NW>::stagger || Ring<PL, NW>::stag2);
         // the source of the chunk after this one (S / KC + 1 of the pass), for FDSRC
         const unsigned short* fdsrc = pbase + (size_t)(S / KC + 1) * (KC * NTO * PL * 512);
         k16_step<NTO, PL, NW, fd, A24>(a, FULL ? 8 : ks, S, kk, last, ci, ring, bias_ring, in, out, slab, ex, bh,
@@ -782,6 +846,18 @@ __device__ __forceinline__ float relu_bit(float v, unsigned& bits) {
         "v_addc_co_u32_e32 %1, vcc, %1, %1, vcc"
         : "+v"(v), "+v"(bits) : : "vcc");
     return v;
+}
+
+// PL = 2, before the head's backward pass (its B operand is the head's G row): column n scaled by
+// 2^(ew - head_col_shift(n)), so that against the column-shifted planes every product carries the
+// layer's 2^ew (the pass unscales as any other); a sigma gradient 2^30 above the rgb ones no longer
+// pushes them out of fp16's range. Lane group g holds columns 4 g + i.
+__device__ __forceinline__ void head_bscale(const K16Args& a, fx4 (&act)[kMaxT]) {
+    const int g = (threadIdx.x & 63) >> 4;
+    const int lm = a.wexp[a.L - 1];
+    const int ew = wshift_of(lm);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) act[0][i] = __builtin_ldexpf(act[0][i], ew - head_col_shift(a.hexp[4 * g + i], lm));
 }
 
 __device__ __forceinline__ void zero_tiles(fx4 (&t)[kMaxT]) {
@@ -926,11 +1002,14 @@ k16_fwd_bwd_kernel(K16Args a) {
             k16_pass<1, PL, NW, false, a24_slabs(PL)>(a, a.ks_f[l], ci, ring, bias_ring, act, out, slab, ex);
             fx4 bv[kMaxT];
             bias_read<1>(std::make_integer_sequence<int, 1>{}, bl, bv);
-            // head pre-activations: features 0..3 = registers 0..3 of lane group 0
+            // head pre-activations: features 0..3 = registers 0..3 of lane group 0; PL = 2 unscales
+            // each column by its own weight shift (head_col_shift)
             if (g == 0) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    comp[ls * 4 + i] = (PL >= 2 ? __builtin_ldexpf(out[0][i], sh) : out[0][i]) + bv[0][i];
+                for (int i = 0; i < 4; ++i) {
+                    const int shi = PL == 2 ? -(ex + head_col_shift(a.hexp[i], a.wexp[l])) : sh;
+                    comp[ls * 4 + i] = (PL >= 2 ? __builtin_ldexpf(out[0][i], shi) : out[0][i]) + bv[0][i];
+                }
             }
         }
     }
@@ -963,7 +1042,14 @@ k16_fwd_bwd_kernel(K16Args a) {
         const unsigned long long mb = mask_w[(size_t)(l - 1) * NW * 64];   // in flight over the pass
         const float xm = sample_max<false>(act);
         store_emin(a, l, exa.get(l), store_sexp(a, l, 1, xm));
-        const int ex = shift_of(xm);
+        int ex = shift_of(xm);
+        if (PL == 2 && l == a.L - 1) {
+            // the head: G's slab as it is (one k-step), then the pass on the column-scaled G row
+            store_slab_step(slab, act[0], act[1]);
+            slab = nullptr;
+            head_bscale(a, act);
+            ex = shift_of(sample_max<false>(act));
+        }
         const int sh = unscale(l, ex);
         k16_hidden_pass<HT, PL, NW>(a, a.ks_b[l], ci, ring, bias_ring, act, out, slab, ex, a.w16 + a.wb_off[l]);
         PROF_ADD(kPfBwd, t_b);
@@ -988,9 +1074,17 @@ k16_fwd_bwd_kernel(K16Args a) {
         zero_tiles(out);
         const float xm = sample_max<false>(act);
         store_emin(a, 0, exa.get(0), store_sexp(a, 0, 1, xm));
-        const int ex = shift_of(xm);
+        int ex = shift_of(xm);
+        float* g0s = g0;
+        if (PL == 2 && a.L == 1) {
+            // a head-only MLP: layer 0 is the head (its column-shifted planes, as above)
+            store_slab_step(g0, act[0], act[1]);
+            g0s = nullptr;
+            head_bscale(a, act);
+            ex = shift_of(sample_max<false>(act));
+        }
         const int sh = unscale(0, ex);
-        k16_pass_n<PL, NW>(a, a.ks_b[0], ci, ring, bias_ring, a.to_b[0], act, out, g0, ex);
+        k16_pass_n<PL, NW>(a, a.ks_b[0], ci, ring, bias_ring, a.to_b[0], act, out, g0s, ex);
         if (valid) {
 #pragma unroll
             for (int o = 0; o < kMaxT; ++o)
@@ -1031,6 +1125,8 @@ struct Pack16Args {
     float* b16;
     int* wexp;   // planes = 2: per-layer max|W| bits (pack16_kernel, from wmax16_kernel partials)
     int* wpart;  // [L][kWmaxParts] partial max|W| bits
+    int* hexp;   // planes = 2: the head's per-column max|W| bits [kHeadCols] (pack16_kernel)
+    int* hpart;  // [kWmaxParts][kHeadCols] their partials (wmax16_kernel)
 };
 
 // planes = 2: max|W_l| as the bits of a non-negative float (integer order = float order), one
@@ -1050,7 +1146,16 @@ __global__ void __launch_bounds__(256) wmax16_kernel(Pack16Args a) {
     if (threadIdx.x == 0)   // fmaxf drops NaNs: the max is finite, +inf or 0
         a.wpart[l * kWmaxParts + blockIdx.x] =
             __float_as_int(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+    // the head's per-column partials (thread j: column j over this block's rows)
+    if (l == a.L - 1 && threadIdx.x < kHeadCols) {
+        const int j = threadIdx.x;
+        float mc = 0.0f;
+        if (j < N)
+            for (int k = blockIdx.x; k < K; k += gridDim.x) mc = fmaxf(mc, fabsf(W[(size_t)k * a.w_n + j]));
+        a.hpart[blockIdx.x * kHeadCols + j] = __float_as_int(mc);
+    }
 }
+
 
 // the layer's max|W| bits from its kWmaxParts partials (uniform per block); block (0, l) also
 // publishes them in wexp[l] for k1
@@ -1067,7 +1172,19 @@ __global__ void pack16_kernel(Pack16Args a) {
     const int l = blockIdx.y;
     const float* W = a.W + (size_t)l * a.w_k * a.w_n;
     const int K = a.k[l], N = a.n[l];
-    const int wsh = a.planes == 2 ? wshift_of(layer_wmax(a, l)) : 0;
+    const int lmax = a.planes == 2 ? layer_wmax(a, l) : 0;
+    const int wsh = a.planes == 2 ? wshift_of(lmax) : 0;
+    const bool head = a.planes == 2 && l == a.L - 1;
+    __shared__ int hsh[kHeadCols];   // the head's per-column shifts
+    if (head) {
+        if (threadIdx.x < kHeadCols) {
+            int mb = 0;
+            for (int i = 0; i < kWmaxParts; ++i) mb = max(mb, a.hpart[i * kHeadCols + threadIdx.x]);
+            hsh[threadIdx.x] = head_col_shift(mb, lmax);
+            if (blockIdx.x == 0) a.hexp[threadIdx.x] = mb;
+        }
+        __syncthreads();
+    }
     const size_t nf = (size_t)a.ks_f[l] * a.to_f[l] * 512, nb = (size_t)a.ks_b[l] * a.to_b[l] * 512;
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < nf + nb + 256;
          e += (size_t)gridDim.x * blockDim.x) {
@@ -1090,7 +1207,7 @@ __global__ void pack16_kernel(Pack16Args a) {
                               ((size_t)(s * to + o) * a.planes) * 512 + ln * 8 + j;
         if (a.planes == 2) {
             _Float16 h, lo;
-            split_h(__builtin_ldexpf(w, wsh), h, lo);
+            split_h(__builtin_ldexpf(w, head && jj < kHeadCols ? hsh[jj] : wsh), h, lo);
             dst[0] = __builtin_bit_cast(unsigned short, h);
             dst[512] = __builtin_bit_cast(unsigned short, lo);
             continue;
@@ -1133,7 +1250,8 @@ unsigned k16_build_knobs() {
            (LNERF_K16_SPLIT_AT != 2 ? kKnobK16SplitAt : 0u) | (LNERF_K16_SCHED != 1 ? kKnobK16Sched : 0u) |
            (LNERF_K16_PRIO != 0 ? kKnobK16Prio : 0u) | (LNERF_K16_SPREAD != 1 ? kKnobK16Spread : 0u) |
            (LNERF_PROF != 0 ? kKnobProf : 0u) | (LNERF_A24 != 1 ? kKnobA24 : 0u) |
-           (LNERF_K16_PIN != 0 ? kKnobK16Pin : 0u) | (LNERF_K16_FDSRC != 0 ? kKnobK16FdSrc : 0u)
+           (LNERF_K16_PIN != 0 ? kKnobK16Pin : 0u) | (LNERF_K16_FDSRC != 0 ? kKnobK16FdSrc : 0u) |
+           (LNERF_K16_STAG2 != 0 ? kKnobK16Stag2 : 0u)
 #ifdef LNERF_K16_ONLY_16_2
            | kKnobK16Only
 #endif
@@ -1169,6 +1287,8 @@ void k16_pack(const FusedPlan& p, const float* ws, const float* bs, hipStream_t 
     a.b16 = p.b16;
     a.wexp = p.wexp16;
     a.wpart = p.wmax_part;
+    a.hexp = p.hexp16;
+    a.hpart = p.wmax_part + (size_t)kMaxLayers * kWmaxParts;
     if (a.planes == 2) wmax16_kernel<<<dim3(kWmaxParts, p.L), 256, 0, s>>>(a);
     size_t nmax = 0;
     for (int l = 0; l < p.L; ++l) {
@@ -1223,6 +1343,7 @@ void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lner
     a.nout = p.n[p.L - 1];
     a.planes = p.x6;
     a.wexp = p.wexp16;
+    a.hexp = p.hexp16;
     a.sexp = p.sexp;
     a.rpad = p.num_wg * p.tile;
     a.epart = p.epart;
@@ -1231,13 +1352,21 @@ void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lner
     {
         const int KC = (p.x6 == 3 || p.tile == 64) ? 1 : 2;
         int ci = 0;
+        // STAG2 (Ring::stag2): chunk c lands in the slot of chunk c - 2, whose last k-step the late
+        // waves have read up to tile half_tiles + kDist when the early waves issue c's pieces: the
+        // early waves take the leading pieces below that point (bits 24..31), the late waves the rest
+        int unread[kMaxChunks] = {};   // per chunk: 1-KiB pieces before its late-unread tail
         auto add = [&](bool fwd, int l) {
             const int ks = fwd ? a.ks_f[l] : a.ks_b[l], to = fwd ? a.to_f[l] : a.to_b[l];
             const size_t per = (size_t)to * a.planes * 512;   // u16 per k-step
+            const int H = to >= 4 ? to * LNERF_K16_SPLIT_AT / 4 : (to + 1) / 2;
             for (int s2 = 0; s2 < ks; s2 += KC, ++ci) {
                 const int nk = ks - s2 < KC ? ks - s2 : KC;
+                const int np = (int)(nk * per * 2 / 1024);
+                unread[ci] = (nk - 1) * to * a.planes + (to < H + kDist ? to : H + kDist) * a.planes;
+                const int early = ci >= 2 ? (np < unread[ci - 2] ? np : unread[ci - 2]) : np;
                 a.chunk_tab[2 * ci] = (unsigned)((fwd ? a.wf_off[l] : a.wb_off[l]) + (size_t)s2 * per);
-                a.chunk_tab[2 * ci + 1] = (unsigned)(nk * per * 2 / 1024) | ((fwd && s2 == 0 ? l + 1 : 0) << 16);
+                a.chunk_tab[2 * ci + 1] = (unsigned)np | ((fwd && s2 == 0 ? l + 1 : 0) << 16) | ((unsigned)early << 24);
             }
         };
         for (int l = 0; l < p.L; ++l) add(true, l);

@@ -21,10 +21,6 @@
 //  * partials per split, summed in order by grad_reduce_kernel (deterministic, no atomics).
 #include "lnerf_internal.h"
 
-#include <stddef.h>
-
-#include <algorithm>
-
 namespace lnerf {
 
 namespace {
@@ -44,14 +40,6 @@ typedef _Float16 hf4 __attribute__((ext_vector_type(4)));
 #ifndef LNERF_DW16_DEPTH
 #define LNERF_DW16_DEPTH 3
 #endif
-// ORDER 1: workgroups dispatched newest-slabs-first -- workgroup b takes the (layer, split) whose
-// sample range k1 wrote last (the tail of the batch: k1's last workgroup round), interleaving the
-// layers, so the first k2 workgroups read slabs still resident in the Infinity Cache; 0: layer by
-// layer, first samples first
-#ifndef LNERF_DW16_ORDER
-#define LNERF_DW16_ORDER 0
-#endif
-constexpr int kMaxMap = 1024;   // workgroups the ORDER map covers (the kernel-argument table)
 
 constexpr int kThreads = 512;
 constexpr int kRows = 512;                  // A rows [0, 256) and G rows [256, 512) of the image
@@ -66,9 +54,16 @@ constexpr int kRows = 512;                  // A rows [0, 256) and G rows [256, 
 constexpr int kImgRow = kRows * 2 + (LNERF_DW16_SWZ ? 0 : 64);
 __host__ __device__ constexpr int swz(int row) { return LNERF_DW16_SWZ ? (0x18140C00 >> (8 * (row & 3))) & 0xFF : 0; }
 constexpr int kPlaneBytes = 16 * kImgRow;
-// PL planes per operand: 3 = bf16x6, 2 = fp16x3, 1 = bf16 (all split x 2^e, per-sample shifts)
+// PL: the split of a dW launch -- 3 = bf16x6, 2 = fp16x3, 1 = bf16 (all x 2^e, per-sample shifts)
+// -- and kHeadX6 = 4: the bf16x6 split on an fp16x3 training's int24 activation slabs, the HEAD
+// layer's dW under fp16x3 (LNERF_DW16_HEADX6): bf16 planes keep fp32's exponent range, so a head G
+// row whose sigma gradient sits 2^30 above its rgb gradients (a tiny sigma behind the delta = 1e8
+// of train_nerf.py:306-311) loses no rgb column to fp16's subnormals
+constexpr int kHeadX6 = 4;
+__host__ __device__ constexpr int nplanes(int PL) { return PL == kHeadX6 ? 3 : PL; }
+__host__ __device__ constexpr bool a24k(int PL) { return PL == kHeadX6 || a24_slabs(PL); }
 template <int PL>
-constexpr int image_bytes() { return PL * kPlaneBytes; }
+constexpr int image_bytes() { return nplanes(PL) * kPlaneBytes; }
 
 struct Dw16Args {
     int kt[kMaxLayers], nt[kMaxLayers];
@@ -89,8 +84,6 @@ struct Dw16Args {
     int rpad;                   // slab positions per layer
     const int* eshift;          // per-layer product shift E_l (k1_reduce_kernel)
     int L;
-    int use_map;                // ORDER: map[blockIdx] = layer << 12 | split
-    unsigned short map[kMaxMap];
 };
 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
@@ -263,7 +256,7 @@ template <int PL>
 __device__ __forceinline__ void sample_scales(unsigned e, int E, float& sa, float& sg) {
     int ea, eg;
     sample_shifts(e, E, ea, eg);
-    if constexpr (a24_slabs(PL)) {
+    if constexpr (a24k(PL)) {
         const int xa = (int)(signed char)(e & 0xFFu);
         ea = xa == -128 ? 0 : ea - (xa == kSexpNonFinite ? 0 : xa) - 8;
     }
@@ -276,7 +269,7 @@ __device__ __forceinline__ void sample_scales(unsigned e, int E, float& sa, floa
 // the test is one wave-uniform branch, taken only when some lane's sample is marked.
 template <int PL>
 __device__ __forceinline__ fx4 round_values(const Loads& L, int i) {
-    if constexpr (a24_slabs(PL)) {
+    if constexpr (a24k(PL)) {
         if (i >= 2) return L.v[i];
         fx4 v = decode_a24(L.v[i]);
         const bool marked = (int)(signed char)(L.e & 0xFFu) == kSexpNonFinite;
@@ -343,12 +336,13 @@ __device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int 
     sa = live ? sa : 0.0f;
     sg = live ? sg : 0.0f;
     const unsigned char* fl = img;
-    bf8 ap[TI][PL];
+    constexpr int NP = nplanes(PL);
+    bf8 ap[TI][NP];
     if constexpr (ACTIVE) {
 #pragma unroll
         for (int i = 0; i < TI; ++i)
 #pragma unroll
-            for (int p = 0; p < PL; ++p) ap[i][p] = read_frag((unsigned char*)fl + p * kPlaneBytes + frag_off(a0 + 32 * i));
+            for (int p = 0; p < NP; ++p) ap[i][p] = read_frag((unsigned char*)fl + p * kPlaneBytes + frag_off(a0 + 32 * i));
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -358,9 +352,9 @@ __device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int 
         if constexpr (ACTIVE) {
             if (k < TJ) {
                 const int j = k < TJ ? k : 0;
-                bf8 gp[PL];
+                bf8 gp[NP];
 #pragma unroll
-                for (int p = 0; p < PL; ++p) gp[p] = read_frag((unsigned char*)fl + p * kPlaneBytes + frag_off(256 + g0 + 32 * j));
+                for (int p = 0; p < NP; ++p) gp[p] = read_frag((unsigned char*)fl + p * kPlaneBytes + frag_off(256 + g0 + 32 * j));
 #pragma unroll
                 for (int i = 0; i < TI; ++i) {
                     fx16 c = acc[i][j];
@@ -398,7 +392,7 @@ __device__ __forceinline__ void hb_step3(const float* A, const float* G, const u
     constexpr int kIB = image_bytes<PL>();
     Loads& fr = I == 0 ? L0 : I == 1 ? L1 : L2;
     const Loads& nx = I == 0 ? L1 : I == 1 ? L2 : L0;
-    issue_loads<a24_slabs(PL)>(A, G, se, kt, nt, m, hb + 3, hb1, fr);
+    issue_loads<a24k(PL)>(A, G, se, kt, nt, m, hb + 3, hb1, fr);
     if (hb + 1 < hb1) {
         dbs[0] += nx.v[2];
         dbs[1] += nx.v[3];
@@ -433,7 +427,7 @@ __device__ __forceinline__ void hb_step2(const float* A, const float* G, const u
     constexpr int kIB = image_bytes<PL>();
     Loads& fr = I == 0 ? L0 : L1;
     const Loads& nx = I == 0 ? L1 : L0;
-    issue_loads<a24_slabs(PL)>(A, G, se, kt, nt, m, hb + 2, hb1, fr);
+    issue_loads<a24k(PL)>(A, G, se, kt, nt, m, hb + 2, hb1, fr);
     if (hb + 1 < hb1) {
         dbs[0] += nx.v[2];
         dbs[1] += nx.v[3];
@@ -485,8 +479,8 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
     const bool full = KT == 8 && NT == 8;
 #if LNERF_DW16_DEPTH == 2
     Loads L0, L1;
-    issue_loads<a24_slabs(PL)>(A, G, se, KT, NT, m, hb0, hb1, L0);
-    issue_loads<a24_slabs(PL)>(A, G, se, KT, NT, m, hb0 + 1, hb1, L1);
+    issue_loads<a24k(PL)>(A, G, se, KT, NT, m, hb0, hb1, L0);
+    issue_loads<a24k(PL)>(A, G, se, KT, NT, m, hb0 + 1, hb1, L1);
     if (hb0 < hb1) {
         dbs[0] += L0.v[2];
         dbs[1] += L0.v[3];
@@ -499,9 +493,9 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
     else hb_loop2<PL, TI, TJ, false, false>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E);
 #else
     Loads L0, L1, L2;
-    issue_loads<a24_slabs(PL)>(A, G, se, KT, NT, m, hb0, hb1, L0);
-    issue_loads<a24_slabs(PL)>(A, G, se, KT, NT, m, hb0 + 1, hb1, L1);
-    issue_loads<a24_slabs(PL)>(A, G, se, KT, NT, m, hb0 + 2, hb1, L2);
+    issue_loads<a24k(PL)>(A, G, se, KT, NT, m, hb0, hb1, L0);
+    issue_loads<a24k(PL)>(A, G, se, KT, NT, m, hb0 + 1, hb1, L1);
+    issue_loads<a24k(PL)>(A, G, se, KT, NT, m, hb0 + 2, hb1, L2);
     if (hb0 < hb1) {
         dbs[0] += L0.v[2];
         dbs[1] += L0.v[3];
@@ -560,22 +554,18 @@ __host__ __device__ __forceinline__ int dw_shape(int kt, int nt) {
 
 template <int PL>
 __global__ void __launch_bounds__(kThreads, 1) dw16_kernel(Dw16Args a) {
-    __shared__ __attribute__((aligned(16))) unsigned char lds[2 * image_bytes<PL>()];
-    int l, sp;
-    if (a.use_map) {
-        // a scalar load from the kernel-argument segment (indexing the by-value table would copy it)
-        const __attribute__((address_space(4))) unsigned short* t =
-            (const __attribute__((address_space(4))) unsigned short*)((const __attribute__((address_space(4))) char*)
-                                                                          __builtin_amdgcn_kernarg_segment_ptr() +
-                                                                      offsetof(Dw16Args, map));
-        const int e = t[blockIdx.x];
-        l = e >> 12;
-        sp = e & 0xFFF;
-    } else {
-        int li = 0;
-        while (li + 1 < a.nl && (int)blockIdx.x >= a.wg_off[li + 1]) ++li;
-        l = a.lid[li];
-        sp = blockIdx.x - a.wg_off[li];
+    // fp16x3 with the head on the bf16x6 split: room for its three planes
+    constexpr bool headx6 = PL == 2 && LNERF_DW16_HEADX6 && a24_slabs(2);
+    __shared__ __attribute__((aligned(16))) unsigned char lds[2 * image_bytes<headx6 ? kHeadX6 : PL>()];
+    int li = 0;
+    while (li + 1 < a.nl && (int)blockIdx.x >= a.wg_off[li + 1]) ++li;
+    const int l = a.lid[li], sp = blockIdx.x - a.wg_off[li];
+    if constexpr (headx6) {
+        // the head (<= 16 outputs: one 32-column tile, kt <= 8: the 1 x 1 shape)
+        if (l == a.L - 1 && dw_shape(a.kt[l], a.nt[l]) == 0) {
+            dw_split<kHeadX6, 1, 1>(a, l, sp, lds);
+            return;
+        }
     }
     switch (dw_shape(a.kt[l], a.nt[l])) {
         case 0: dw_split<PL, 1, 1>(a, l, sp, lds); break;
@@ -632,7 +622,7 @@ __global__ void __launch_bounds__(1024) k1_reduce_kernel(const int* __restrict__
 unsigned dw16_build_knobs() {
     return (LNERF_DW16_SPLIT_LATE != 1 ? kKnobDwSplitLate : 0u) | (LNERF_DW16_DEPTH != 3 ? kKnobDwDepth : 0u) |
            (LNERF_DW16_SWZ != 1 ? kKnobDwSwz : 0u) | (LNERF_A24 != 1 ? kKnobA24 : 0u) |
-           (LNERF_DW16_ORDER != 0 ? kKnobDwOrder : 0u);
+           (LNERF_DW16_HEADX6 != 1 || LNERF_DW16_HEAD_WEIGHT != 2 ? kKnobDwHeadX6 : 0u);
 }
 
 void dw16_launch(const FusedPlan& p, hipStream_t s) {
@@ -659,21 +649,6 @@ void dw16_launch(const FusedPlan& p, hipStream_t s) {
     a.rpad = p.num_wg * p.tile;
     a.eshift = p.dw_shift;
     a.L = p.L;
-    if (LNERF_DW16_ORDER == 1 && p.dw_grid <= kMaxMap) {
-        // newest slabs first: key (sp + 1/2) / splits_l, descending (k1's workgroups run in blockIdx
-        // order, so the last sample ranges were written last), layers interleaved at equal keys
-        struct E {
-            double key;
-            int l, sp;
-        };
-        E e[kMaxMap];
-        int n = 0;
-        for (int l = 0; l < p.L; ++l)
-            for (int sp = 0; sp < p.dw_splits[l]; ++sp) e[n++] = E{(sp + 0.5) / p.dw_splits[l], l, sp};
-        std::stable_sort(e, e + n, [](const E& x, const E& y) { return x.key > y.key; });
-        for (int i = 0; i < n; ++i) a.map[i] = (unsigned short)(e[i].l << 12 | e[i].sp);
-        a.use_map = n == p.dw_grid ? 1 : 0;
-    }
     static_assert(sizeof(Dw16Args) <= 4096, "kernel arguments");
     // the per-layer product shifts of k1_reduce_launch (launched right after k1)
     if (p.x6 == 2) dw16_kernel<2><<<p.dw_grid, kThreads, 0, s>>>(a);

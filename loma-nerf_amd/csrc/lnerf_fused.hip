@@ -177,12 +177,16 @@ void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S, bool train, int
     // each one streams (kt + nt tiles per 32-sample block): the kernel is bandwidth-bound, so
     // equal bytes per workgroup balance it. One partial per split.
     const int grid = dw_grid > 0 ? (dw_grid < 16 ? 16 : dw_grid > 4096 ? 4096 : dw_grid) : kDefaultDwGrid;
+    // (the head weighted for its bf16x6 split under fp16x3, LNERF_DW16_HEAD_WEIGHT; every precision
+    // shares the layout so that the workspace size does not depend on it)
+    const int hw = LNERF_DW16_HEADX6 ? LNERF_DW16_HEAD_WEIGHT : 1;
+    auto weight = [&](int l) { return (kt[l] + nt[l]) * (l == L - 1 ? hw : 1); };
     int tiles_sum = 0;
-    for (int l = 0; l < L; ++l) tiles_sum += kt[l] + nt[l];
+    for (int l = 0; l < L; ++l) tiles_sum += weight(l);
     size_t dwp = 0, dbp = 0;
     int wg = 0;
     for (int l = 0; l < L; ++l) {
-        int sp = (int)((long long)grid * (kt[l] + nt[l]) / tiles_sum);
+        int sp = (int)((long long)grid * weight(l) / tiles_sum);
         sp = sp < 1 ? 1 : sp;
         sp = sp > y.blocks ? y.blocks : sp;
         y.splits[l] = sp;

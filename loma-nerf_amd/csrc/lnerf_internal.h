@@ -13,6 +13,15 @@ namespace lnerf {
 constexpr int kWmaxParts = 32;   // blocks per layer of the max|W| pass before the fp16x3 packing
 constexpr int kHeadCols = 16;    // head columns with their own fp16x3 weight shift (k16 head outputs)
 constexpr int kDefaultDwGrid = 512;   // dW workgroups per step unless LNERF_OPT_DW_GRID says otherwise
+// fp16x3 training runs the head's dW on the bf16x6 split (lnerf_dw16.hip kHeadX6), twice the
+// MFMAs and a heavier split per sample: the head gets LNERF_DW16_HEAD_WEIGHT x its byte share of
+// the dW workgroups (make_layout), so its splits do not finish last
+#ifndef LNERF_DW16_HEADX6
+#define LNERF_DW16_HEADX6 1
+#endif
+#ifndef LNERF_DW16_HEAD_WEIGHT
+#define LNERF_DW16_HEAD_WEIGHT 2
+#endif
 
 // ---- fp16x3 exponent shifts ------------------------------------------------------------------
 // The shift e that puts a group's largest magnitude m in [2^13, 2^14) for the fp16 hi/lo split
@@ -68,8 +77,7 @@ enum : unsigned {
     kKnobK16FullDma = 1u << 0, kKnobK16KDist = 1u << 1, kKnobK16SplitAt = 1u << 2, kKnobK16Sched = 1u << 3,
     kKnobK16Prio = 1u << 4, kKnobK16Spread = 1u << 5, kKnobProf = 1u << 6, kKnobA24 = 1u << 7,
     kKnobK16Only = 1u << 8, kKnobDwSplitLate = 1u << 9, kKnobDwDepth = 1u << 10, kKnobDwSwz = 1u << 11,
-    kKnobK16Pin = 1u << 12, kKnobK16FdSrc = 1u << 13, kKnobDwOrder = 1u << 14, kKnobKrStagger = 1u << 15,
-    kKnobK16Stag2 = 1u << 16,
+    kKnobK16Pin = 1u << 12, kKnobK16FdSrc = 1u << 13, kKnobKrStagger = 1u << 15, kKnobDwHeadX6 = 1u << 17,
 };
 unsigned k16_build_knobs();
 unsigned dw16_build_knobs();

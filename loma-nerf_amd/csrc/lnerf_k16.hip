@@ -43,10 +43,6 @@ constexpr int kWaves = 8;                     // the most waves per workgroup
 constexpr int kMaxChunks = 2 * kMaxLayers * 8 + 1;   // <= 2 passes x 8 k-steps per layer + 1 end
 constexpr int kMaxT = 16;                     // 16-feature tiles per 256-wide layer
 constexpr int kCompBytes = 2688 * 4;          // composite_tile's scratch (comp[0, 2688))
-// staggered wave pairs for fp16x3 on the 2-slot ring (Ring::stag2)
-#ifndef LNERF_K16_STAG2
-#define LNERF_K16_STAG2 0
-#endif
 // full hidden passes get compile-time step bounds and test-free DMA issue (A/B: 0 = generic only)
 #ifndef LNERF_K16_FULLDMA
 #define LNERF_K16_FULLDMA 1
@@ -66,14 +62,8 @@ constexpr int kCompBytes = 2688 * 4;          // composite_tile's scratch (comp[
 template <int PL, int NW = 8>
 struct Ring {
     static constexpr int KC = (PL == 3 || NW == 4) ? 1 : 2;
-    // STAG2 (fp16x3, 8 waves): staggered wave pairs on the 2-slot ring of 2-k-step chunks. Waves 4-7
-    // meet each chunk's barrier after half of its last k-step's tiles, so they still read the tail of
-    // chunk c - 1 while chunk c + 1 lands in its slot: the early waves (0-3) DMA only the leading
-    // pieces of chunk c + 1 that the late waves have read already (ChunkT::early, from the chunk
-    // table), the late waves the rest once they are past chunk c - 1 (LNERF_K16_STAG2)
-    static constexpr bool stag2 = LNERF_K16_STAG2 && PL == 2 && NW == 8;
-    static constexpr bool stagger = (PL == 3 && NW == 8) || stag2;
-    static constexpr int slots = (PL == 3 && NW == 8) ? 3 : 2;
+    static constexpr bool stagger = PL == 3 && NW == 8;
+    static constexpr int slots = stagger ? 3 : 2;
     static constexpr int slot_bytes = KC * kMaxT * PL * 1024;
     static constexpr int off_comp = slots * slot_bytes;
     static constexpr int off_ray = off_comp + kCompBytes;
@@ -178,7 +168,6 @@ struct ChunkT {
     const unsigned short* src;   // nullptr: past the last chunk
     int bytes;
     int bias;                    // layer whose biases ride with this chunk, -1: none
-    int early;                   // STAG2: leading 1-KiB pieces the early waves may DMA (k16_launch)
 };
 
 __device__ __forceinline__ ChunkT chunk_at(const K16Args& a, int ci) {
@@ -188,7 +177,7 @@ __device__ __forceinline__ ChunkT chunk_at(const K16Args& a, int ci) {
                                                             offsetof(K16Args, chunk_tab)) + 2 * ci;
     const unsigned off = t[0], e = t[1];
     const int bytes = (int)(e & 0xFFFFu) * 1024;
-    return ChunkT{bytes ? a.w16 + off : nullptr, bytes, (int)((e >> 16) & 0xFFu) - 1, (int)(e >> 24)};
+    return ChunkT{bytes ? a.w16 + off : nullptr, bytes, (int)(e >> 16) - 1};
 }
 
 // LDS-DMA (global_load_lds_dwordx4) of a chunk into its ring slot: 8 KiB per round of the
@@ -368,18 +357,19 @@ __device__ __forceinline__ void read_tile(const unsigned char* base, bf8 (&w)[3]
 #ifndef LNERF_K16_SPREAD
 #define LNERF_K16_SPREAD 1
 #endif
-// PIN: the next k-step's operand split and this k-step's int24 slab packing are pinned between
-// the two halves of the output tiles (an empty asm that "reads and writes" their registers),
-// where the partner wave's MFMAs cover them; without it the compiler sinks both next to their
-// first use, at the k-step boundary, where both waves of a SIMD issue them together
+// PIN 2: the next k-step's operand split and this k-step's int24 slab packing run as VALU fillers
+// spread over the first 12 of 16 output tiles (FillSpread), each result pinned there by an empty
+// asm that "reads and writes" its registers in place; 0: the compiler sinks both next to their
+// first use, at the k-step boundary, where both waves of a SIMD issue them together (round 5,
+// interleaved A/B with FDSRC: k1 1.33-1.35 ms against 1.36-1.39)
 #ifndef LNERF_K16_PIN
-#define LNERF_K16_PIN 0
+#define LNERF_K16_PIN 2
 #endif
 // FDSRC: a whole chunk of a full pass takes its source address from the pass base (an SGPR the
 // layer loop loads once) instead of the chunk table (a scalar load + lgkmcnt(0) per chunk, right
 // after the barrier)
 #ifndef LNERF_K16_FDSRC
-#define LNERF_K16_FDSRC 0
+#define LNERF_K16_FDSRC 1
 #endif
 constexpr int kPiecesMax = 8;   // pieces per wave of a full chunk (64 KiB / 8 waves, 32 KiB / 4)
 struct DmaJob {
@@ -387,20 +377,17 @@ struct DmaJob {
     unsigned char* dst = nullptr;   // LDS address of this wave's piece 0
     int n = 0;                   // this wave's pieces of the chunk
 };
-// piece p of a job: STRIDE KiB apart (NW for the round-robin assignment; 4 for STAG2's, where the
-// four early or the four late waves share a chunk)
-template <int STRIDE>
+template <int NW>
 __device__ __forceinline__ void dma_piece(const DmaJob& j, int p) {
     const int lane = threadIdx.x & 63;
-    glds16(j.src + p * (STRIDE * 1024) + lane * 16, lds_addr(j.dst + p * (STRIDE * 1024)));
+    glds16(j.src + p * (NW * 1024) + lane * 16, lds_addr(j.dst + p * (NW * 1024)));
 }
-// the pieces that land on output tile O: p with p * NTO / NP == O (all on tile 0 when NTO == 1);
-// FULL: the chunk is known to be whole (every wave issues NP pieces, no per-piece test)
-template <int NTO, int O, int STRIDE, bool FULL, int NP, int... P>
+// the pieces that land on output tile O: p with p * NTO / kPiecesMax == O (all on tile 0 when NTO == 1);
+// FULL: the chunk is known to be whole (every wave issues kPiecesMax pieces, no per-piece test)
+template <int NTO, int O, int NW, bool FULL, int... P>
 __device__ __forceinline__ void dma_pieces_at(const DmaJob& j, std::integer_sequence<int, P...>) {
-    (((P * NTO) / NP == O ? ((FULL || P < j.n) ? dma_piece<STRIDE>(j, P) : void()) : void()), ...);
+    (((P * NTO) / kPiecesMax == O ? ((FULL || P < j.n) ? dma_piece<NW>(j, P) : void()) : void()), ...);
 }
-constexpr int kPiecesStag = 16;   // STAG2: at most 13 pieces per wave, one per output tile
 
 // Output tile O of one k-step: issue the reads of tile O + kDist, the MFMAs of tile O (small
 // terms first; the compiler waits for tile O's reads only, lgkmcnt(N) with the younger ones in
@@ -411,6 +398,14 @@ template <int NTO>
 constexpr int half_tiles() {
     return NTO >= 4 ? NTO * LNERF_K16_SPLIT_AT / 4 : (NTO + 1) / 2;
 }
+
+// The staggered wave pairs (bf16x6) branch on the wave's half right after a k-step's MFMAs (the
+// late or the early barrier); on the short side of that branch the compiler's hazard padding has
+// come up short (tests/test_isa.py: a VALU write 2 wait states after an MFMA reading the register as
+// C, an MFMA result read 4-7 states after issue). 16 wait states here, on every path, cover any
+// MFMA of the kernel. The statement takes the last tile's accumulator in place, so that tile's
+// MFMAs cannot be scheduled below it (in-place operand, no instruction writes it).
+__device__ __forceinline__ void mfma_branch_guard(fx4& acc) { asm volatile("s_nop 7\n\ts_nop 7" : "+v"(acc)::"memory"); }
 
 // no VALU filler between the tiles (see FillSpread)
 struct NoFill {
@@ -423,17 +418,8 @@ __device__ __forceinline__ void tile_step(const unsigned char* base, bf8 (&w)[kD
                                           const bf8& bm, const bf8& bl, fx4 (&out)[kMaxT], const DmaJob& job,
                                           F& fill) {
     if constexpr (O + kDist < NTO) read_tile<PL, O + kDist>(base, w[(O + kDist) % (kDist + 1)]);
-    if constexpr (Ring<PL, NW>::stag2) {
-        // over the first half_tiles only: a late wave of a one-k-step chunk meets the barrier there,
-        // and every piece must be older than its vmcnt
-        constexpr int HT2 = half_tiles<NTO>() < 1 ? 1 : half_tiles<NTO>();
-        if constexpr (O < HT2)
-            if (job.n) dma_pieces_at<HT2, O, 4, false, kPiecesStag>(job, std::make_integer_sequence<int, kPiecesStag>{});
-    } else if constexpr (FD) {
-        dma_pieces_at<NTO, O, NW, true, kPiecesMax>(job, std::make_integer_sequence<int, kPiecesMax>{});
-    } else if (job.n) {
-        dma_pieces_at<NTO, O, NW, false, kPiecesMax>(job, std::make_integer_sequence<int, kPiecesMax>{});
-    }
+    if constexpr (FD) dma_pieces_at<NTO, O, NW, true>(job, std::make_integer_sequence<int, kPiecesMax>{});
+    else if (job.n) dma_pieces_at<NTO, O, NW, false>(job, std::make_integer_sequence<int, kPiecesMax>{});
     // keep tile O + kDist's reads ahead of tile O's MFMAs: the machine scheduler otherwise sinks
     // each read next to its first consumer (one MFMA of slack, an LDS round trip exposed per tile);
     // the compiler still places every wait itself
@@ -560,7 +546,7 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
     const int lane = threadIdx.x & 63;
     const unsigned char* base = ring + (ci % R::slots) * R::slot_bytes + kk * NTO * PL * 1024 + lane * 16;
     const bool st = slab != nullptr;
-    constexpr bool spread = LNERF_K16_SPREAD && (!R::stagger || R::stag2);
+    constexpr bool spread = LNERF_K16_SPREAD && !R::stagger;
     DmaJob job;
     if (kk == 0) {
         // DMA of chunk ci + 1 (its table entry is a scalar load the compiler waits for with
@@ -568,31 +554,11 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
         // now, before the first weight tiles; spread: one piece per kPiecesMax-th of the output
         // tiles, between the MFMAs. The barrier waits for this wave's pieces of chunk ci + 1 only:
         // the slab stores issued after them (two per k-step) stay in flight.
-        // FDSRC: the next chunk of this full pass, whole, no biases (fdsrc = its source); under STAG2
-        // only from the pass's second chunk on (the slot's previous chunk is then this pass's, so the
-        // early waves' share is kStag2Early; the first chunk's predecessor is the previous pass's)
-        constexpr int kStag2H = half_tiles<NTO>();
-        constexpr int kStag2Early = (R::KC - 1) * NTO * PL + (NTO < kStag2H + kDist ? NTO : kStag2H + kDist) * PL;
-        const bool fdtab = FD && LNERF_K16_FDSRC && (!R::stag2 || s >= R::KC);
-        const ChunkT c = fdtab ? ChunkT{fdsrc, KC_BYTES, -1, kStag2Early} : chunk_at(a, ci + 1);
+        // FDSRC: the next chunk of this full pass, whole, no biases (fdsrc = its source)
+        const ChunkT c = (FD && LNERF_K16_FDSRC) ? ChunkT{fdsrc, KC_BYTES, -1} : chunk_at(a, ci + 1);
         unsigned char* dst = ring + ((ci + 1) % R::slots) * R::slot_bytes;
         int issued;
-        if constexpr (R::stag2) {
-            // early waves: pieces e, e + 4, ... below c.early; late waves: the same residues above it
-            const int wave = wave_id(), e4 = wave & 3;
-            const int np = c.src ? c.bytes / 1024 : 0;
-            const int E = c.early < np ? c.early : np;
-            const int q0 = wave < 4 ? e4 : E + ((e4 - E) & 3);
-            const int q1 = wave < 4 ? E : np;
-            job.n = q0 < q1 ? (q1 - q0 + 3) / 4 : 0;
-            job.src = (const char*)c.src + q0 * 1024;
-            job.dst = dst + q0 * 1024;
-            issued = job.n;
-            if (c.bias >= 0 && wave == NW - 1) {
-                glds16(a.b16 + (size_t)c.bias * 256 + lane * 4, lds_addr(bias_ring + (c.bias % 3) * 256));
-                ++issued;
-            }
-        } else if constexpr (spread) {
+        if constexpr (spread) {
             const int wave = wave_id();
             const int woff = wave * 1024;
             job.n = FD ? kPiecesMax
@@ -618,11 +584,9 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
     if constexpr (NTO > 1) read_tile<PL, 1>(base, w[1]);
     if constexpr (NTO > 2 && kDist > 2) read_tile<PL, 2>(base, w[2]);
     static_assert(kDist == 2 || kDist == 3, "the prologue reads kDist tiles");
-    Packed24 pk{};
     auto store = [&]() {
         if constexpr (A24) {
-            if constexpr (LNERF_K16_PIN == 1) store_packed24((unsigned char*)slab + s * 3072, pk);
-            else store_slab_step24((unsigned char*)slab + s * 3072, in[2 * s], in[2 * s + 1], ex);
+            store_slab_step24((unsigned char*)slab + s * 3072, in[2 * s], in[2 * s + 1], ex);
         } else {
             store_slab_step(slab + s * 1024, in[2 * s], in[2 * s + 1]);
         }
@@ -632,7 +596,7 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
     // the next prologue's critical path), second half, [spread: the slab stores, younger than
     // every piece], [early: barrier]
     constexpr int H = half_tiles<NTO>();   // split after tile H
-    constexpr bool spread_fill = LNERF_K16_PIN == 2 && PL == 2 && NTO == 16 && (!R::stagger || R::stag2);
+    constexpr bool spread_fill = LNERF_K16_PIN == 2 && PL == 2 && NTO == 16 && !R::stagger;
     // a late wave meets the barrier before this k-step's spread slab stores: they are not pending yet
     const int late_pending = (st && spread && pending >= 2) ? pending - 2 : pending;
     if constexpr (spread_fill) {
@@ -661,28 +625,16 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
     }
     NoFill nf;
     tile_steps<NTO, PL, NW, FD, 0>(std::make_integer_sequence<int, H>{}, base, w, bh, bm, bl, out, job, nf);
+    if constexpr (R::stagger) mfma_branch_guard(out[H > 0 ? H - 1 : 0]);
     if (late && last) dma_barrier(late_pending);
     bf8 nh = {}, nm = {}, nl = {};
     if (s + 1 < ks) make_b<PL>(in, s + 1 < 8 ? s + 1 : 0, ex, nh, nm, nl);
-    if constexpr (LNERF_K16_PIN == 1) {
-        if (s + 1 < ks) {
-            pin(nh);
-            if constexpr (PL >= 2) pin(nm);
-            if constexpr (PL == 3) pin(nl);
-        }
-        if constexpr (A24) {
-            if (st && spread) {
-                pk = pack_slab_step24(in[2 * s], in[2 * s + 1], ex);
-                pin(pk.p0);
-                pin(pk.p1);
-            }
-        }
-    }
     tile_steps<NTO, PL, NW, FD, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, bh, bm, bl, out, job, nf);
     if (st && spread) {
         asm volatile("" ::: "memory");
         store();
     }
+    if constexpr (R::stagger) mfma_branch_guard(out[NTO - 1]);
     if (!late && last) dma_barrier(pending);
     if (last) ++ci;
     bh = nh;
@@ -703,8 +655,7 @@ __device__ __forceinline__ void k16_pass_step(const K16Args& a, int ks, int& ci,
         constexpr int kk = S % KC;
         const bool last = kk == KC - 1 || (FULL ? S == 7 : S + 1 == ks);
         constexpr bool fd = LNERF_K16_FULLDMA && FULL && kk == 0 && S / KC + 1 < 8 / KC &&
-                            KC * NTO * PL == kPiecesMax * NW && LNERF_K16_SPREAD &&
-                            (!Ring<PL, NW>::stagger || Ring<PL, NW>::stag2);
+                            KC * NTO * PL == kPiecesMax * NW && LNERF_K16_SPREAD && !Ring<PL, NW>::stagger;
         // the source of the chunk after this one (S / KC + 1 of the pass), for FDSRC
         const unsigned short* fdsrc = pbase + (size_t)(S / KC + 1) * (KC * NTO * PL * 512);
         k16_step<NTO, PL, NW, fd, A24>(a, FULL ? 8 : ks, S, kk, last, ci, ring, bias_ring, in, out, slab, ex, bh,
@@ -1250,8 +1201,7 @@ unsigned k16_build_knobs() {
            (LNERF_K16_SPLIT_AT != 2 ? kKnobK16SplitAt : 0u) | (LNERF_K16_SCHED != 1 ? kKnobK16Sched : 0u) |
            (LNERF_K16_PRIO != 0 ? kKnobK16Prio : 0u) | (LNERF_K16_SPREAD != 1 ? kKnobK16Spread : 0u) |
            (LNERF_PROF != 0 ? kKnobProf : 0u) | (LNERF_A24 != 1 ? kKnobA24 : 0u) |
-           (LNERF_K16_PIN != 0 ? kKnobK16Pin : 0u) | (LNERF_K16_FDSRC != 0 ? kKnobK16FdSrc : 0u) |
-           (LNERF_K16_STAG2 != 0 ? kKnobK16Stag2 : 0u)
+           (LNERF_K16_PIN != 2 ? kKnobK16Pin : 0u) | (LNERF_K16_FDSRC != 1 ? kKnobK16FdSrc : 0u)
 #ifdef LNERF_K16_ONLY_16_2
            | kKnobK16Only
 #endif
@@ -1352,21 +1302,13 @@ void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lner
     {
         const int KC = (p.x6 == 3 || p.tile == 64) ? 1 : 2;
         int ci = 0;
-        // STAG2 (Ring::stag2): chunk c lands in the slot of chunk c - 2, whose last k-step the late
-        // waves have read up to tile half_tiles + kDist when the early waves issue c's pieces: the
-        // early waves take the leading pieces below that point (bits 24..31), the late waves the rest
-        int unread[kMaxChunks] = {};   // per chunk: 1-KiB pieces before its late-unread tail
         auto add = [&](bool fwd, int l) {
             const int ks = fwd ? a.ks_f[l] : a.ks_b[l], to = fwd ? a.to_f[l] : a.to_b[l];
             const size_t per = (size_t)to * a.planes * 512;   // u16 per k-step
-            const int H = to >= 4 ? to * LNERF_K16_SPLIT_AT / 4 : (to + 1) / 2;
             for (int s2 = 0; s2 < ks; s2 += KC, ++ci) {
                 const int nk = ks - s2 < KC ? ks - s2 : KC;
-                const int np = (int)(nk * per * 2 / 1024);
-                unread[ci] = (nk - 1) * to * a.planes + (to < H + kDist ? to : H + kDist) * a.planes;
-                const int early = ci >= 2 ? (np < unread[ci - 2] ? np : unread[ci - 2]) : np;
                 a.chunk_tab[2 * ci] = (unsigned)((fwd ? a.wf_off[l] : a.wb_off[l]) + (size_t)s2 * per);
-                a.chunk_tab[2 * ci + 1] = (unsigned)np | ((fwd && s2 == 0 ? l + 1 : 0) << 16) | ((unsigned)early << 24);
+                a.chunk_tab[2 * ci + 1] = (unsigned)(nk * per * 2 / 1024) | ((fwd && s2 == 0 ? l + 1 : 0) << 16);
             }
         };
         for (int l = 0; l < p.L; ++l) add(true, l);

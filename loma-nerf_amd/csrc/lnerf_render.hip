@@ -45,7 +45,7 @@ constexpr int kMaxChunks = kMaxLayers * 4 + 1;   // <= 4 chunks per forward pass
 // the partner's MFMAs instead of in lockstep with them (MI355X_MICROARCH.md, two waves per SIMD,
 // item 9). The late waves still read chunk c - 1 while chunk c + 1 lands: three ring slots.
 #ifndef LNERF_KR_STAGGER
-#define LNERF_KR_STAGGER 0
+#define LNERF_KR_STAGGER 1
 #endif
 constexpr int kSlots = LNERF_KR_STAGGER ? 3 : 2;
 constexpr int kOffComp = kSlots * kSlot;         // the ring
@@ -367,7 +367,7 @@ kr_fwd_kernel(KrArgs a) {
 // plain bf16, the NeRF head, whole rays of <= 128 samples, a layer-0 input of <= 64 features
 // (PE with F <= 10); anything else renders on k16's forward
 // compile-time settings of this object that differ from the product build (lnerf_build_knobs)
-unsigned kr_build_knobs() { return LNERF_KR_STAGGER != 0 ? kKnobKrStagger : 0u; }
+unsigned kr_build_knobs() { return LNERF_KR_STAGGER != 1 ? kKnobKrStagger : 0u; }
 
 bool kr_supported(const FusedPlan& p) {
     return p.x6 == 1 && !p.head_fit && p.S <= 128 && p.n[p.L - 1] <= 16 && p.tile == 128 && p.k[0] <= 64;

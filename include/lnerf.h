@@ -146,9 +146,13 @@ enum {
                                  (e.g. a dW column whose G values sit 1e-9 below the row's other
                                  columns keeps ~2 % -- tests/test_gpu_edge.py fp16x3_dw_bound;
                                  LNERF_MFMA_BF16X6 has fp32's exponent range and no such limit).
+                                 The head's weights carry a shift per output column and, in
+                                 training, its dW runs on the bf16x6 split, so rgb and sigma
+                                 adjoints far apart (delta = 1e8 rays) keep their own ranges.
                                  Training in fp16x3 keeps the activations it hands from the
                                  forward to the dW pass as int24 (x rounded to a multiple of
-                                 2^-23 of its row's max|x|), inside the same row-relative bound. */
+                                 2^-23 of its row's max|x|), inside the same row-relative bound;
+                                 a row holding NaN/inf is marked and reaches dW as NaN.        */
     LNERF_MFMA_BF16X6 = 512,  /* fused path: the bf16x6 split (x = hi+mid+lo in bf16, six bf16
                                  MFMAs per product, dropped terms <= 2^-24 |w x|)              */
     LNERF_K32 = 2048,         /* removed in round 4 (it lost to k16): an error                 */

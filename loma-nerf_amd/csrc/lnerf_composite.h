@@ -224,6 +224,84 @@ __device__ __forceinline__ float composite_tile(const A& a, int wg, float* comp,
     return 0.0f;
 }
 
+// ---- forward-only compositing for the render (kr): composite_tile's per-sample expressions and
+// results, with each along-ray scan done inside the wave (shuffles, log2 64 steps) plus one carry
+// across the waves a ray spans (its earlier waves' partials through LDS): two workgroup barriers
+// instead of composite_tile's 2 (log2 S + 1). The products and sums associate differently from
+// composite_tile's LDS rounds (and from loma's sequential loops), at fp32 rounding level. Threads
+// 0..TS-1 own one sample each; z [TS][4] at comp[0], the wave partials [TS / 64][4] at comp[4 TS].
+template <int TS, class A>
+__device__ __forceinline__ void composite_fwd_wave(const A& a, int wg, float* comp, float* rayloss) {
+    static_assert(TS % 64 == 0, "whole waves of samples");
+    const int tid = threadIdx.x, S = a.S, lane = tid & 63, wv = tid >> 6;
+    float* c_z = comp;
+    float* pub = comp + 4 * TS;
+    const bool act = tid < TS;
+    const int ls = act ? tid : 0;
+    const int rl = ls / S, j = ls - rl * S;   // ray within the tile, sample within the ray
+    const int ray = wg * a.rpw + rl;
+    const int ntile = a.rpw * S;
+    const bool valid = act && ls < ntile && ray < a.rays;
+    const size_t gs = (size_t)ray * S + j;
+    float rgb[3] = {0, 0, 0}, al = 0, cc = 1;
+    if (valid) {
+        float z[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) z[k] = c_z[ls * 4 + k];
+        // head activation (nerf.py:153-167): channel 3 ReLU, 0..2 sigmoid
+#pragma unroll
+        for (int k = 0; k < 3; ++k) rgb[k] = 1.0f / (1.0f + expf(0.0f - z[k]));
+        const float sigma = (z[3] > 0.0f) ? z[3] : 0.0f;
+        const float delta = a.dists ? a.dists[gs] : ray_delta(j, S, a.near_t, a.far_t);
+        al = 1.0f - expf((0.0f - sigma) * delta);
+        cc = (1.0f - al) + (float)(1e-10);
+    }
+    const int jw = j < lane ? j : lane;        // this ray's samples before this one in this wave
+    const int ws = (ls - j) >> 6;              // the wave holding the ray's first sample
+    // P_j, the inclusive product (nerf.py:226-272): in-wave, then the earlier waves' partials
+    float P = cc;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const float o = __shfl_up(P, d, 64);
+        if (jw >= d) P = o * P;
+    }
+    if (act && lane == 63) pub[wv * 4] = P;
+    __syncthreads();
+    if (act)
+        for (int w = wv - 1; w >= ws; --w) P = pub[w * 4] * P;
+    const float T = (j == 0) ? 1.0f : P;
+    const float wgt = al * T;
+    // colour: the segmented sum of w rgb, read at the ray's last sample
+    float cv[3] = {wgt * rgb[0], wgt * rgb[1], wgt * rgb[2]};
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float o = __shfl_up(cv[k], d, 64);
+            if (jw >= d) cv[k] = o + cv[k];
+        }
+    }
+    if (act && lane == 63)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) pub[wv * 4 + 1 + k] = cv[k];
+    __syncthreads();
+    if (act && j == S - 1 && ls < ntile) {
+        for (int w = wv - 1; w >= ws; --w)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) cv[k] = pub[w * 4 + 1 + k] + cv[k];
+        float loss = 0.0f;
+        if (valid) {
+            const float* t = a.target + (size_t)ray * 3;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                loss = loss + (cv[k] - t[k]) * (cv[k] - t[k]);
+                if (a.acc_color) a.acc_color[(size_t)ray * 3 + k] = cv[k];
+            }
+        }
+        rayloss[rl] = loss;
+    }
+}
+
 // ---- the mlp_fit head (scripts/mlp_fit.py:120-145, fit_img.py:423-532) for one tile ----------
 // One thread per row (S = 1, so a "ray" is a row): sigmoid on each of the nout <= 4 head outputs
 // (mlp_fit.py:127-132: 1 / (1 + exp(0 - x))), loss = sum_c (o_c - t_c)^2 (mlp_fit.py:140-145;

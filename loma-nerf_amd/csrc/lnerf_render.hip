@@ -40,22 +40,28 @@ constexpr int kMaxT = 16;                        // 16-wide output tiles of a 25
 constexpr int kKC = 2;                           // k-steps per chunk
 constexpr int kSlot = kKC * kMaxT * 1024;        // one chunk: 2 k-steps x 16 tiles x 1 KiB
 constexpr int kMaxChunks = kMaxLayers * 4 + 1;   // <= 4 chunks per forward pass + the end marker
-// STAGGER: waves 4-7 (each the SIMD partner of wave w - 4) meet each chunk's barrier half a k-step
-// later than waves 0-3 (in the middle of the chunk's last k-step), so the two waves of a SIMD run
-// their chunk prologues and layer epilogues (bias + ReLU + bf16 conversion of 128 values) beside
-// the partner's MFMAs instead of in lockstep with them (MI355X_MICROARCH.md, two waves per SIMD,
-// item 9). The late waves still read chunk c - 1 while chunk c + 1 lands: three ring slots.
-#ifndef LNERF_KR_STAGGER
-#define LNERF_KR_STAGGER 1
-#endif
-constexpr int kSlots = LNERF_KR_STAGGER ? 3 : 2;
+// Staggered wave pairs: waves 4-7 (each the SIMD partner of wave w - 4) meet each chunk's barrier
+// half a k-step later than waves 0-3 (in the middle of the chunk's last k-step), so the two waves of
+// a SIMD run their chunk prologues and layer epilogues (bias + ReLU + bf16 conversion of 128 values)
+// beside the partner's MFMAs instead of in lockstep with them (MI355X_MICROARCH.md, two waves per
+// SIMD, item 9). The late waves still read chunk c - 1 while chunk c + 1 lands: three ring slots.
+// (Round 5: 63.4 -> 61.6 ms per frame against the unstaggered 2-slot ring, which is gone.)
+constexpr int kSlots = 3;
+// The head's weights (<= 8 k-steps x one 16-wide tile, 8 KiB) and biases stay resident in LDS,
+// loaded at the start beside chunk 0: the head pass runs with no DMA and no barrier, and chunk 0 is
+// issued before the encoding (whose scratch sits in ring slot 2) so it lands while the encoding
+// runs (round 5: with the in-wave compositing, 55.5 -> 53.7 ms per frame).
 constexpr int kOffComp = kSlots * kSlot;         // the ring
 constexpr int kOffRay = kOffComp + comp::kCompFloats * kTile * 4;
-constexpr int kOffBias = kOffRay + kTile * 4;
-constexpr int kLds = kOffBias + 3 * 256 * 4;     // + a 3-slot ring of layer biases
+constexpr int kOffBias = kOffRay + kTile * 4;    // a 3-slot ring of layer biases
+constexpr int kOffHead = kOffBias + 3 * 256 * 4; // the resident head: 8 KiB of weights, 1 KiB of biases
+constexpr int kLds = kOffHead + 9 * 1024;
 static_assert(kLds <= 160 * 1024, "LDS budget");
 constexpr int kPePerWave = 16 * 65 * 4;          // the encoding scratch of one wave (16 samples)
-static_assert(kWaves * kPePerWave <= 2 * kSlot, "the encoding scratch lives in the ring");
+// the encoding scratch: from ring slot 2 on into the idle compositing scratch (chunk 0 lands in
+// slot 0 meanwhile; slot 2 is first written by chunk 2's DMA, issued after the first chunk barrier)
+constexpr int kOffPe = 2 * kSlot;
+static_assert(kOffPe + kWaves * kPePerWave <= kOffRay, "encoding scratch");
 
 struct KrArgs {
     int L;
@@ -66,6 +72,8 @@ struct KrArgs {
     // the chunk stream: per chunk {u16 offset in w16, (bytes / 1024) | (bias layer + 1) << 16},
     // zero past the end; read with scalar loads from the kernel-argument segment
     unsigned chunk_tab[2 * kMaxChunks];
+    unsigned head_off;         // u16 offset of the head's packed weights in w16 (not in the chunk
+                               // stream: resident)
     int rays, S, rpw, R, input_mode, F;
     float near_t, far_t;
     const float* x;
@@ -220,12 +228,6 @@ __device__ __forceinline__ void kr_tile(const unsigned char* base, bf8 (&w)[kDis
     acc[1][O] = mfma(f, b1, acc[1][O]);
 }
 
-template <int NTO, int... O>
-__device__ __forceinline__ void kr_tiles(std::integer_sequence<int, O...>, const unsigned char* base,
-                                         bf8 (&w)[kDist + 1], const bf8& b0, const bf8& b1,
-                                         fx4 (&acc)[kGroups][kMaxT], const Job& job) {
-    (kr_tile<NTO, O>(base, w, b0, b1, acc, job), ...);
-}
 // tiles B, B + 1, ... of one k-step
 template <int NTO, int B, int... O>
 __device__ __forceinline__ void kr_tiles_from(std::integer_sequence<int, O...>, const unsigned char* base,
@@ -250,22 +252,32 @@ __device__ __forceinline__ void kr_step(const KrArgs& a, int ks, int& ci, unsign
 #pragma unroll
     for (int o = 0; o < kDist; ++o)
         if (o < NTO) w[o] = *(const bf8*)(base + o * 1024);
-    if constexpr (LNERF_KR_STAGGER) {
-        // late waves: the barrier after the first half of the last k-step's tiles
-        constexpr int H = NTO / 2;
-        const bool late = wave_id() >= 4;
-        kr_tiles_from<NTO, 0>(std::make_integer_sequence<int, H>{}, base, w, B[0][S], B[1][S], acc, job);
-        if (last && late) chunk_barrier();
-        kr_tiles_from<NTO, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, B[0][S], B[1][S], acc, job);
-        if (last && !late) chunk_barrier();
-        if (last) ++ci;
-        return;
+    // late waves: the barrier after the first half of the last k-step's tiles
+    constexpr int H = NTO / 2;
+    const bool late = wave_id() >= 4;
+    kr_tiles_from<NTO, 0>(std::make_integer_sequence<int, H>{}, base, w, B[0][S], B[1][S], acc, job);
+    if (last && late) chunk_barrier();
+    kr_tiles_from<NTO, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, B[0][S], B[1][S], acc, job);
+    if (last && !late) chunk_barrier();
+    if (last) ++ci;
+}
+
+// the head pass from the resident weights (k-step s at head + s KiB): no DMA, no barrier
+__device__ __forceinline__ void kr_head_resident(int ks, const unsigned char* head, const bf8 (&B)[kGroups][8],
+                                                 fx4 (&acc)[kGroups][kMaxT]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        if (s < ks) {
+            const bf8 f = *(const bf8*)(head + s * 1024 + lane * 16);
+            acc[0][0] = mfma(f, B[0][s], acc[0][0]);
+            acc[1][0] = mfma(f, B[1][s], acc[1][0]);
+        }
     }
-    kr_tiles<NTO>(std::make_integer_sequence<int, NTO>{}, base, w, B[0][S], B[1][S], acc, job);
-    if (last) {
-        chunk_barrier();
-        ++ci;
-    }
+    // the compiler pads no MFMA hazard on the branch out of the conditional k-steps (tests/test_isa.py
+    // found the bias add 7 states after the last MFMA): 16 wait states cover any MFMA result, in
+    // place on both accumulators so no MFMA is scheduled below this point
+    asm volatile("s_nop 7\n\ts_nop 7" : "+v"(acc[0][0]), "+v"(acc[1][0])::"memory");
 }
 
 template <int NTO, int... S>
@@ -321,6 +333,20 @@ kr_fwd_kernel(KrArgs a) {
     const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
 #endif
     KR_PROF_T(t_start);
+    int ci = 0;
+    {
+        // chunk 0 (layer 0's weights and biases) and the resident head, issued first: they land
+        // while the encoding runs (waited for by the first chunk barrier)
+        const Job j0 = chunk_job(a, 0, ring, bias_ring);
+        job_piece<0>(j0);
+        job_piece<1>(j0);
+        job_piece<2>(j0);
+        job_piece<3>(j0);
+        if (wave < a.ks[a.L - 1])
+            glds16((const char*)(a.w16 + a.head_off) + wave * 1024 + lane * 16, lds_addr(lds + kOffHead + wave * 1024));
+        if (wave == kWaves - 2)
+            glds16(a.b16 + (size_t)(a.L - 1) * 256 + lane * 4, lds_addr(lds + kOffHead + 8 * 1024));
+    }
 
     // ---- layer-0 input (k0 <= 64: two k-steps) as bf16 B operands, group by group, through a
     // per-wave LDS scratch [16 samples][65]: POINTS / RAYS encode one lane per (sample,
@@ -329,7 +355,7 @@ kr_fwd_kernel(KrArgs a) {
 #pragma unroll
     for (int G = 0; G < kGroups; ++G) {
         constexpr int kStride = 65;
-        float* pe = (float*)ring + wave * (16 * kStride);
+        float* pe = (float*)(lds + kOffPe) + wave * (16 * kStride);
         const int lbase = wave * 32 + G * 16;                 // local sample of the group's row 0
         const int tile_base = wg * tile_samples + lbase;
         if (a.input_mode != LNERF_INPUT_ENCODED) {
@@ -358,19 +384,13 @@ kr_fwd_kernel(KrArgs a) {
             B[G][s] = v;
         }
     }
-    __syncthreads();   // the first DMA overwrites the scratch
+    // each wave read only its own scratch rows (LDS operations of a wave complete in order)
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
     KR_PROF_ADD(kRpPE, t_start);
     KR_PROF_T(t_d);
 
-    int ci = 0;
-    {
-        const Job j0 = chunk_job(a, 0, ring, bias_ring);
-        job_piece<0>(j0);
-        job_piece<1>(j0);
-        job_piece<2>(j0);
-        job_piece<3>(j0);
-        chunk_barrier();
-    }
+    chunk_barrier();
     KR_PROF_ADD(kRpDma0, t_d);
 
     fx4 acc[kGroups][kMaxT];
@@ -391,11 +411,11 @@ kr_fwd_kernel(KrArgs a) {
             KR_PROF_ADD(kRpEpi, t_e);
         } else {
             KR_PROF_T(t_h);
-            kr_pass<1>(std::make_integer_sequence<int, 8>{}, a, ks, ci, ring, bias_ring, B, acc);
+            kr_head_resident(ks, lds + kOffHead, B, acc);
             KR_PROF_ADD(kRpHead, t_h);
             // head pre-activations (features 0..3: registers 0..3 of lane group 0), after the sum
             if (g == 0) {
-                const fx4 b = *(const fx4*)bl;
+                const fx4 b = *(const fx4*)(lds + kOffHead + 8 * 1024);
 #pragma unroll
                 for (int G = 0; G < kGroups; ++G) {
                     const int ls = wave * 32 + G * 16 + n;
@@ -408,7 +428,7 @@ kr_fwd_kernel(KrArgs a) {
     KR_PROF_ADD(kRpLoop, t_loop);
     KR_PROF_T(t_c);
     __syncthreads();
-    comp::composite_tile<kTile>(a, wg, comp, rayloss, false);
+    comp::composite_fwd_wave<kTile>(a, wg, comp, rayloss);
     __syncthreads();
     if (tid == 0) {
         float lsum = 0.0f;
@@ -429,7 +449,7 @@ kr_fwd_kernel(KrArgs a) {
 // (PE with F <= 10); anything else renders on k16's forward
 // compile-time settings of this object that differ from the product build (lnerf_build_knobs)
 unsigned kr_build_knobs() {
-    return (LNERF_KR_STAGGER != 1 ? kKnobKrStagger : 0u) | (LNERF_KR_SCHED != 1 ? kKnobKrSched : 0u) |
+    return (LNERF_KR_SCHED != 1 ? kKnobKrSched : 0u) |
            (LNERF_KR_DIST != 2 ? kKnobKrDist : 0u) | (LNERF_PE_DOUBLING != 1 ? kKnobPeDoubling : 0u) |
            (LNERF_PROF != 0 ? kKnobProf : 0u);
 }
@@ -466,7 +486,9 @@ void kr_launch(const FusedPlan& p, const lnerf_batch& b, const lnerf_outputs& ou
     a.seed = 1.0f;
     // the forward chunk stream of k16_pack's one-plane packing: 2 k-steps per chunk
     int ci = 0;
-    for (int l = 0; l < p.L; ++l) {
+    // the head is not in the chunk stream (the kernel loads it at its start)
+    a.head_off = (unsigned)p.w16f_off[p.L - 1];
+    for (int l = 0; l < p.L - 1; ++l) {
         const size_t per = (size_t)p.to16_f[l] * 512;   // u16 per k-step
         for (int s2 = 0; s2 < p.ks16_f[l]; s2 += kKC, ++ci) {
             const int nk = p.ks16_f[l] - s2 < kKC ? p.ks16_f[l] - s2 : kKC;

@@ -302,6 +302,165 @@ __device__ __forceinline__ void composite_fwd_wave(const A& a, int wg, float* co
     }
 }
 
+// ---- composite_tile with the along-ray scans inside the wave (training, k1): the same per-sample
+// expressions and outputs (z in at comp[0], gz out at comp[4 TS], rayloss, acc_color, d_target,
+// d_dists), the forward scans as in composite_fwd_wave and the reverse suffix scan of
+// G_j = a_j + c_{j+1} G_{j+1} by shuffles down plus the later waves' partials: four workgroup
+// barriers instead of composite_tile's 3 log2(S) + 4. LDS: wave partials [TS / 64][8] at 8 TS,
+// c_j at 9 TS, P_j at 10 TS, per-ray dacc [rays][4] at 11 TS (within kCompFloats = 21 per sample).
+template <int TS, class A>
+__device__ __forceinline__ void composite_tile_wave(const A& a, int wg, float* comp, float* rayloss, bool grad) {
+    static_assert(TS % 64 == 0, "whole waves of samples");
+    const int tid = threadIdx.x, S = a.S, lane = tid & 63, wv = tid >> 6;
+    float* c_z = comp;
+    float* c_gz = comp + 4 * TS;
+    float* pub = comp + 8 * TS;
+    float* c_cc = comp + 9 * TS;
+    float* c_P = comp + 10 * TS;
+    float* c_ray = comp + 11 * TS;
+    const bool act = tid < TS;
+    const int ls = act ? tid : 0;
+    const int rl = ls / S, j = ls - rl * S;   // ray within the tile, sample within the ray
+    const int ray = wg * a.rpw + rl;
+    const int ntile = a.rpw * S;
+    const bool valid = act && ls < ntile && ray < a.rays;
+    const size_t gs = (size_t)ray * S + j;
+    float z[4] = {0, 0, 0, 0}, rgb[3] = {0, 0, 0}, sigma = 0, delta = 0, al = 0, cc = 1;
+    if (valid) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) z[k] = c_z[ls * 4 + k];
+        // head activation (nerf.py:153-167): channel 3 ReLU, 0..2 sigmoid
+#pragma unroll
+        for (int k = 0; k < 3; ++k) rgb[k] = 1.0f / (1.0f + expf(0.0f - z[k]));
+        sigma = (z[3] > 0.0f) ? z[3] : 0.0f;
+        delta = a.dists ? a.dists[gs] : ray_delta(j, S, a.near_t, a.far_t);
+        al = 1.0f - expf((0.0f - sigma) * delta);
+        cc = (1.0f - al) + (float)(1e-10);
+    }
+    const int jw = j < lane ? j : lane;        // this ray's samples before this one in this wave
+    const int ws = (ls - j) >> 6;              // the wave holding the ray's first sample
+    // P_j, the inclusive product (nerf.py:226-272)
+    float P = cc;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const float o = __shfl_up(P, d, 64);
+        if (jw >= d) P = o * P;
+    }
+    if (act) {
+        if (lane == 63) pub[wv * 8] = P;
+        c_cc[ls] = cc;
+    }
+    __syncthreads();
+    if (act) {
+        for (int w = wv - 1; w >= ws; --w) P = pub[w * 8] * P;
+        c_P[ls] = P;
+    }
+    const float T = (j == 0) ? 1.0f : P;
+    const float wgt = al * T;
+    // colour: the segmented sum of w rgb, read at the ray's last sample
+    float cv[3] = {wgt * rgb[0], wgt * rgb[1], wgt * rgb[2]};
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float o = __shfl_up(cv[k], d, 64);
+            if (jw >= d) cv[k] = o + cv[k];
+        }
+    }
+    if (act && lane == 63)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) pub[wv * 8 + 1 + k] = cv[k];
+    __syncthreads();
+    if (act && j == S - 1 && ls < ntile) {
+        for (int w = wv - 1; w >= ws; --w)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) cv[k] = pub[w * 8 + 1 + k] + cv[k];
+        float loss = 0.0f;
+        if (valid) {
+            const float* t = a.target + (size_t)ray * 3;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                loss = loss + (cv[k] - t[k]) * (cv[k] - t[k]);
+                if (a.acc_color) a.acc_color[(size_t)ray * 3 + k] = cv[k];
+            }
+            if (grad) {
+                // reverse of the loss (lg_composite_bwd_kernel): dacc = 2 seed (C - t)
+                for (int k = 2; k >= 0; --k) {
+                    const float a1 = (cv[k] - t[k]) * a.seed;
+                    const float a2 = 0.0f - ((cv[k] - t[k]) * a.seed);
+                    c_ray[rl * 4 + k] = 0.0f + a1 + a1;
+                    if (a.d_target) a.d_target[(size_t)ray * 3 + k] = (0.0f + a2) + a2;
+                }
+            }
+        }
+        rayloss[rl] = loss;
+    }
+    if (!grad) return;
+    __syncthreads();
+
+    // ---- reverse, per sample ----
+    float dacc[3] = {0, 0, 0}, dw = 0.0f, drgb[4] = {0, 0, 0, 0};
+    if (valid) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) dacc[k] = c_ray[rl * 4 + k];
+        for (int k = 2; k >= 0; --k) {
+            dw += rgb[k] * dacc[k];
+            drgb[k] += wgt * dacc[k];
+        }
+    }
+    float dal = T * dw;
+    // G_j = a_j + c_{j+1} G_{j+1}: the suffix composition of (a, b) pairs, in-wave, then the later
+    // waves' partials (their lane 0's composition; the ray's last sample has b = 0)
+    float ga = (j >= 1) ? al * dw : 0.0f;
+    float gb = (valid && j + 1 < S) ? c_cc[ls + 1] : 0.0f;
+    const int rest = S - 1 - j, lrest = 63 - lane;
+    const int je = rest < lrest ? rest : lrest;   // this ray's samples after this one in this wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const float oa = __shfl_down(ga, d, 64), ob = __shfl_down(gb, d, 64);
+        if (je >= d) {
+            ga = ga + gb * oa;
+            gb = gb * ob;
+        }
+    }
+    if (act && lane == 0) {
+        pub[wv * 8 + 4] = ga;
+        pub[wv * 8 + 5] = gb;
+    }
+    __syncthreads();
+    const int we = (ls - j + S - 1) >> 6;      // the wave holding the ray's last sample
+    if (act && we > wv) {
+        float gn = 0.0f;
+        for (int w = we; w > wv; --w) gn = pub[w * 8 + 4] + pub[w * 8 + 5] * gn;
+        ga = ga + gb * gn;
+    }
+    if (valid) {
+        const float dc = (j >= 1) ? c_P[ls - 1] * ga : ga;
+        dal += 0.0f - dc;                                       // cC = (1 - al) + 1e-10
+        const float adj2 = (0.0f - dal) * expf((0.0f - sigma) * delta);   // alpha reverse
+        drgb[3] += 0.0f - (delta * adj2);
+        if (a.d_dists) a.d_dists[gs] = 0.0f + (0.0f - sigma) * adj2;
+        // head activation reverse (reverse_diff.py Div/exp/Sub rules; ReLU on the post value)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float dz = drgb[k];
+            float g;
+            if (k == 3) {
+                g = (sigma > 0.0f) ? dz : 0.0f;
+            } else {
+                const float x = z[k];
+                const float u = 1.0f + expf(0.0f - x);
+                const float adj_div = ((0.0f - dz) * 1.0f) / (u * u);
+                g = 0.0f + (0.0f - adj_div * expf(0.0f - x));
+            }
+            c_gz[ls * 4 + k] = g;
+        }
+    } else if (act) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) c_gz[ls * 4 + k] = 0.0f;
+    }
+}
+
 // ---- the mlp_fit head (scripts/mlp_fit.py:120-145, fit_img.py:423-532) for one tile ----------
 // One thread per row (S = 1, so a "ray" is a row): sigmoid on each of the nout <= 4 head outputs
 // (mlp_fit.py:127-132: 1 / (1 + exp(0 - x))), loss = sum_c (o_c - t_c)^2 (mlp_fit.py:140-145;

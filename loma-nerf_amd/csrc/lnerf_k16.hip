@@ -371,6 +371,27 @@ __device__ __forceinline__ void read_tile(const unsigned char* base, bf8 (&w)[3]
 #ifndef LNERF_K16_FDSRC
 #define LNERF_K16_FDSRC 1
 #endif
+// SPREAD2: a whole chunk of a full pass (FD) spreads its 8 pieces per wave over BOTH k-steps of
+// the chunk before (pieces 0-3 between the first k-step's tiles, 4-7 between the second's) instead
+// of 8 between the first k-step's 16 tiles
+// ONECHUNK: a one-tile pass (the head's forward; hidden layers <= 16 wide) streams all its <= 8
+// k-steps as ONE chunk (<= 8 PL KiB), one barrier instead of ks / KC, each waiting on a DMA issued
+// only a few MFMAs earlier
+#ifndef LNERF_K16_ONECHUNK
+#define LNERF_K16_ONECHUNK 0
+#endif
+// k-steps per chunk of a pass with NTO output tiles (k16_launch's chunk table follows the same rule)
+template <int NTO, int PL, int NW>
+constexpr int pass_kc() {
+    return (LNERF_K16_ONECHUNK && NTO == 1) ? 8 : Ring<PL, NW>::KC;
+}
+// WAVECOMP: the compositing's along-ray scans in-wave (comp::composite_tile_wave)
+#ifndef LNERF_K16_WAVECOMP
+#define LNERF_K16_WAVECOMP 0
+#endif
+#ifndef LNERF_K16_SPREAD2
+#define LNERF_K16_SPREAD2 0
+#endif
 constexpr int kPiecesMax = 8;   // pieces per wave of a full chunk (64 KiB / 8 waves, 32 KiB / 4)
 struct DmaJob {
     const char* src = nullptr;   // the wave's (uniform) address of piece 0
@@ -387,6 +408,13 @@ __device__ __forceinline__ void dma_piece(const DmaJob& j, int p) {
 template <int NTO, int O, int NW, bool FULL, int... P>
 __device__ __forceinline__ void dma_pieces_at(const DmaJob& j, std::integer_sequence<int, P...>) {
     (((P * NTO) / kPiecesMax == O ? ((FULL || P < j.n) ? dma_piece<NW>(j, P) : void()) : void()), ...);
+}
+// SPREAD2: half HALF (pieces 4 HALF .. 4 HALF + 3) of a whole chunk: the first half on tiles
+// q NTO / 4 of the chunk's first k-step, the second on tiles q NTO / 8 of its last (the first half of
+// that k-step, so the pieces land before the barrier at its end)
+template <int NTO, int O, int NW, int HALF, int... Q>
+__device__ __forceinline__ void dma_pieces_half(const DmaJob& j, std::integer_sequence<int, Q...>) {
+    (((Q * NTO) / (HALF ? 8 : 4) == O ? dma_piece<NW>(j, 4 * HALF + Q) : void()), ...);
 }
 
 // Output tile O of one k-step: issue the reads of tile O + kDist, the MFMAs of tile O (small
@@ -413,12 +441,15 @@ struct NoFill {
     __device__ __forceinline__ void at() {}
 };
 
-template <int NTO, int PL, int NW, bool FD, int O, typename F = NoFill>
+// FDP: how this k-step issues the next chunk's DMA: 0 generic (per-piece tests), 3 a whole chunk's
+// 8 pieces, 1 / 2 its first / second half (SPREAD2)
+template <int NTO, int PL, int NW, int FDP, int O, typename F = NoFill>
 __device__ __forceinline__ void tile_step(const unsigned char* base, bf8 (&w)[kDist + 1][3], const bf8& bh,
                                           const bf8& bm, const bf8& bl, fx4 (&out)[kMaxT], const DmaJob& job,
                                           F& fill) {
     if constexpr (O + kDist < NTO) read_tile<PL, O + kDist>(base, w[(O + kDist) % (kDist + 1)]);
-    if constexpr (FD) dma_pieces_at<NTO, O, NW, true>(job, std::make_integer_sequence<int, kPiecesMax>{});
+    if constexpr (FDP == 3) dma_pieces_at<NTO, O, NW, true>(job, std::make_integer_sequence<int, kPiecesMax>{});
+    else if constexpr (FDP == 1 || FDP == 2) dma_pieces_half<NTO, O, NW, FDP - 1>(job, std::make_integer_sequence<int, 4>{});
     else if (job.n) dma_pieces_at<NTO, O, NW, false>(job, std::make_integer_sequence<int, kPiecesMax>{});
     // keep tile O + kDist's reads ahead of tile O's MFMAs: the machine scheduler otherwise sinks
     // each read next to its first consumer (one MFMA of slack, an LDS round trip exposed per tile);
@@ -446,11 +477,11 @@ __device__ __forceinline__ void tile_step(const unsigned char* base, bf8 (&w)[kD
 }
 
 // tiles B, B+1, ... of one k-step
-template <int NTO, int PL, int NW, bool FD, int B, typename F, int... O>
+template <int NTO, int PL, int NW, int FDP, int B, typename F, int... O>
 __device__ __forceinline__ void tile_steps(std::integer_sequence<int, O...>, const unsigned char* base,
                                            bf8 (&w)[kDist + 1][3], const bf8& bh, const bf8& bm,
                                            const bf8& bl, fx4 (&out)[kMaxT], const DmaJob& job, F& fill) {
-    (tile_step<NTO, PL, NW, FD, B + O>(base, w, bh, bm, bl, out, job, fill), ...);
+    (tile_step<NTO, PL, NW, FDP, B + O>(base, w, bh, bm, bl, out, job, fill), ...);
 }
 
 // LNERF_K16_PIN = 2 (fp16x3, 16 output tiles): the next k-step's operand split and this k-step's
@@ -536,7 +567,7 @@ __device__ __forceinline__ void make_b(const fx4 (&in)[kMaxT], int s, int ex, bf
 // (the A_{l-1} or G_l slab of this wave's half-block).
 // FD: this k-step issues the DMA of a chunk known to be whole (the next chunk of the same full
 // pass): kPiecesMax pieces per wave with no per-piece test and no byte arithmetic.
-template <int NTO, int PL, int NW, bool FD = false, bool A24 = false>
+template <int NTO, int PL, int NW, int FDP = 0, bool A24 = false>
 __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk, bool last, int& ci,
                                          unsigned char* ring, float* bias_ring, const fx4 (&in)[kMaxT],
                                          fx4 (&out)[kMaxT], float* __restrict__ slab, int ex, bf8& bh,
@@ -547,8 +578,9 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
     const unsigned char* base = ring + (ci % R::slots) * R::slot_bytes + kk * NTO * PL * 1024 + lane * 16;
     const bool st = slab != nullptr;
     constexpr bool spread = LNERF_K16_SPREAD && !R::stagger;
+    constexpr bool FD = FDP != 0;
     DmaJob job;
-    if (kk == 0) {
+    if (kk == 0 || FDP == 2) {
         // DMA of chunk ci + 1 (its table entry is a scalar load the compiler waits for with
         // lgkmcnt(0), so it is read before the fragment reads are issued). Unspread: every piece
         // now, before the first weight tiles; spread: one piece per kPiecesMax-th of the output
@@ -608,9 +640,9 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
         f.pack = A24 && st && spread;
         f.s = s;
         f.ex = ex;
-        tile_steps<NTO, PL, NW, FD, 0>(std::make_integer_sequence<int, H>{}, base, w, bh, bm, bl, out, job, f);
+        tile_steps<NTO, PL, NW, FDP, 0>(std::make_integer_sequence<int, H>{}, base, w, bh, bm, bl, out, job, f);
         if (late && last) dma_barrier(late_pending);
-        tile_steps<NTO, PL, NW, FD, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, bh, bm, bl, out, job, f);
+        tile_steps<NTO, PL, NW, FDP, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, bh, bm, bl, out, job, f);
         if (st && spread) {
             asm volatile("" ::: "memory");
             if constexpr (A24) store_packed24((unsigned char*)slab + s * 3072, f.pk);
@@ -624,12 +656,12 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
         return;
     }
     NoFill nf;
-    tile_steps<NTO, PL, NW, FD, 0>(std::make_integer_sequence<int, H>{}, base, w, bh, bm, bl, out, job, nf);
+    tile_steps<NTO, PL, NW, FDP, 0>(std::make_integer_sequence<int, H>{}, base, w, bh, bm, bl, out, job, nf);
     if constexpr (R::stagger) mfma_branch_guard(out[H > 0 ? H - 1 : 0]);
     if (late && last) dma_barrier(late_pending);
     bf8 nh = {}, nm = {}, nl = {};
     if (s + 1 < ks) make_b<PL>(in, s + 1 < 8 ? s + 1 : 0, ex, nh, nm, nl);
-    tile_steps<NTO, PL, NW, FD, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, bh, bm, bl, out, job, nf);
+    tile_steps<NTO, PL, NW, FDP, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, bh, bm, bl, out, job, nf);
     if (st && spread) {
         asm volatile("" ::: "memory");
         store();
@@ -650,12 +682,13 @@ __device__ __forceinline__ void k16_pass_step(const K16Args& a, int ks, int& ci,
                                               float* bias_ring, const fx4 (&in)[kMaxT], fx4 (&out)[kMaxT],
                                               float* __restrict__ slab, int ex, bf8& bh, bf8& bm, bf8& bl,
                                               int& pending, const unsigned short* pbase) {
-    constexpr int KC = Ring<PL, NW>::KC;
+    constexpr int KC = pass_kc<NTO, PL, NW>();
     if (FULL || S < ks) {
         constexpr int kk = S % KC;
         const bool last = kk == KC - 1 || (FULL ? S == 7 : S + 1 == ks);
-        constexpr bool fd = LNERF_K16_FULLDMA && FULL && kk == 0 && S / KC + 1 < 8 / KC &&
-                            KC * NTO * PL == kPiecesMax * NW && LNERF_K16_SPREAD && !Ring<PL, NW>::stagger;
+        constexpr bool whole_next = LNERF_K16_FULLDMA && FULL && S / KC + 1 < 8 / KC &&
+                                    KC * NTO * PL == kPiecesMax * NW && LNERF_K16_SPREAD && !Ring<PL, NW>::stagger;
+        constexpr int fd = !whole_next ? 0 : !(LNERF_K16_SPREAD2 && KC == 2) ? (kk == 0 ? 3 : 0) : kk + 1;
         // the source of the chunk after this one (S / KC + 1 of the pass), for FDSRC
         const unsigned short* fdsrc = pbase + (size_t)(S / KC + 1) * (KC * NTO * PL * 512);
         k16_step<NTO, PL, NW, fd, A24>(a, FULL ? 8 : ks, S, kk, last, ci, ring, bias_ring, in, out, slab, ex, bh,
@@ -960,6 +993,7 @@ k16_fwd_bwd_kernel(K16Args a) {
 
     // ---- rendering + loss + rendering reverse (one thread per sample, scans along rays) ----
     if (a.head_fit) comp::fit_tile(a, wg, comp, rayloss, st, a.nout);
+    else if (LNERF_K16_WAVECOMP) comp::composite_tile_wave<comp::kTileSamples>(a, wg, comp, rayloss, st);
     else comp::composite_tile(a, wg, comp, rayloss, st);
     __syncthreads();
     if (tid == 0) {
@@ -1193,6 +1227,8 @@ unsigned k16_build_knobs() {
            (LNERF_K16_PRIO != 0 ? kKnobK16Prio : 0u) | (LNERF_K16_SPREAD != 1 ? kKnobK16Spread : 0u) |
            (LNERF_PROF != 0 ? kKnobProf : 0u) | (LNERF_A24 != 1 ? kKnobA24 : 0u) |
            (LNERF_K16_PIN != 2 ? kKnobK16Pin : 0u) | (LNERF_K16_FDSRC != 1 ? kKnobK16FdSrc : 0u) |
+           (LNERF_K16_SPREAD2 != 0 ? kKnobK16Spread2 : 0u) | (LNERF_K16_ONECHUNK != 0 ? kKnobK16OneChunk : 0u) |
+           (LNERF_K16_WAVECOMP != 0 ? kKnobK16WaveComp : 0u) |
            (LNERF_PE_DOUBLING != 1 ? kKnobPeDoubling : 0u)
 #ifdef LNERF_K16_ONLY_16_2
            | kKnobK16Only
@@ -1292,10 +1328,11 @@ void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lner
     // the chunk stream: forward 0..L-1, backward L-1..1 (training), backward 0 (d_x); chunks of
     // KC k-steps (Ring: 2 for fp16x3 / bf16, 1 for bf16x6), the pack layout's consecutive k-steps
     {
-        const int KC = (p.x6 == 3 || p.tile == 64) ? 1 : 2;
+        const int KC0 = (p.x6 == 3 || p.tile == 64) ? 1 : 2;
         int ci = 0;
         auto add = [&](bool fwd, int l) {
             const int ks = fwd ? a.ks_f[l] : a.ks_b[l], to = fwd ? a.to_f[l] : a.to_b[l];
+            const int KC = (LNERF_K16_ONECHUNK && to == 1) ? 8 : KC0;   // pass_kc
             const size_t per = (size_t)to * a.planes * 512;   // u16 per k-step
             for (int s2 = 0; s2 < ks; s2 += KC, ++ci) {
                 const int nk = ks - s2 < KC ? ks - s2 : KC;

@@ -371,26 +371,21 @@ __device__ __forceinline__ void read_tile(const unsigned char* base, bf8 (&w)[3]
 #ifndef LNERF_K16_FDSRC
 #define LNERF_K16_FDSRC 1
 #endif
-// SPREAD2: a whole chunk of a full pass (FD) spreads its 8 pieces per wave over BOTH k-steps of
-// the chunk before (pieces 0-3 between the first k-step's tiles, 4-7 between the second's) instead
-// of 8 between the first k-step's 16 tiles
 // ONECHUNK: a one-tile pass (the head's forward; hidden layers <= 16 wide) streams all its <= 8
-// k-steps as ONE chunk (<= 8 PL KiB), one barrier instead of ks / KC, each waiting on a DMA issued
-// only a few MFMAs earlier
+// k-steps as ONE chunk (<= 8 PL KiB), one barrier instead of ks / KC, each of which waited on a DMA
+// issued only a few MFMAs earlier (round 5, in-process interleaved A/B: k1 -0.9 %)
 #ifndef LNERF_K16_ONECHUNK
-#define LNERF_K16_ONECHUNK 0
+#define LNERF_K16_ONECHUNK 1
 #endif
 // k-steps per chunk of a pass with NTO output tiles (k16_launch's chunk table follows the same rule)
 template <int NTO, int PL, int NW>
 constexpr int pass_kc() {
     return (LNERF_K16_ONECHUNK && NTO == 1) ? 8 : Ring<PL, NW>::KC;
 }
-// WAVECOMP: the compositing's along-ray scans in-wave (comp::composite_tile_wave)
+// WAVECOMP: the compositing's along-ray scans in-wave (comp::composite_tile_wave: 4 workgroup
+// barriers instead of 3 log2 S + 4; round 5: k1 -0.2 %, with ONECHUNK -1.1 %)
 #ifndef LNERF_K16_WAVECOMP
-#define LNERF_K16_WAVECOMP 0
-#endif
-#ifndef LNERF_K16_SPREAD2
-#define LNERF_K16_SPREAD2 0
+#define LNERF_K16_WAVECOMP 1
 #endif
 constexpr int kPiecesMax = 8;   // pieces per wave of a full chunk (64 KiB / 8 waves, 32 KiB / 4)
 struct DmaJob {
@@ -408,13 +403,6 @@ __device__ __forceinline__ void dma_piece(const DmaJob& j, int p) {
 template <int NTO, int O, int NW, bool FULL, int... P>
 __device__ __forceinline__ void dma_pieces_at(const DmaJob& j, std::integer_sequence<int, P...>) {
     (((P * NTO) / kPiecesMax == O ? ((FULL || P < j.n) ? dma_piece<NW>(j, P) : void()) : void()), ...);
-}
-// SPREAD2: half HALF (pieces 4 HALF .. 4 HALF + 3) of a whole chunk: the first half on tiles
-// q NTO / 4 of the chunk's first k-step, the second on tiles q NTO / 8 of its last (the first half of
-// that k-step, so the pieces land before the barrier at its end)
-template <int NTO, int O, int NW, int HALF, int... Q>
-__device__ __forceinline__ void dma_pieces_half(const DmaJob& j, std::integer_sequence<int, Q...>) {
-    (((Q * NTO) / (HALF ? 8 : 4) == O ? dma_piece<NW>(j, 4 * HALF + Q) : void()), ...);
 }
 
 // Output tile O of one k-step: issue the reads of tile O + kDist, the MFMAs of tile O (small
@@ -442,14 +430,13 @@ struct NoFill {
 };
 
 // FDP: how this k-step issues the next chunk's DMA: 0 generic (per-piece tests), 3 a whole chunk's
-// 8 pieces, 1 / 2 its first / second half (SPREAD2)
+// 8 pieces (round 5: spreading them over both k-steps of the chunk measured +0.3 % in k1)
 template <int NTO, int PL, int NW, int FDP, int O, typename F = NoFill>
 __device__ __forceinline__ void tile_step(const unsigned char* base, bf8 (&w)[kDist + 1][3], const bf8& bh,
                                           const bf8& bm, const bf8& bl, fx4 (&out)[kMaxT], const DmaJob& job,
                                           F& fill) {
     if constexpr (O + kDist < NTO) read_tile<PL, O + kDist>(base, w[(O + kDist) % (kDist + 1)]);
     if constexpr (FDP == 3) dma_pieces_at<NTO, O, NW, true>(job, std::make_integer_sequence<int, kPiecesMax>{});
-    else if constexpr (FDP == 1 || FDP == 2) dma_pieces_half<NTO, O, NW, FDP - 1>(job, std::make_integer_sequence<int, 4>{});
     else if (job.n) dma_pieces_at<NTO, O, NW, false>(job, std::make_integer_sequence<int, kPiecesMax>{});
     // keep tile O + kDist's reads ahead of tile O's MFMAs: the machine scheduler otherwise sinks
     // each read next to its first consumer (one MFMA of slack, an LDS round trip exposed per tile);
@@ -580,7 +567,7 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
     constexpr bool spread = LNERF_K16_SPREAD && !R::stagger;
     constexpr bool FD = FDP != 0;
     DmaJob job;
-    if (kk == 0 || FDP == 2) {
+    if (kk == 0) {
         // DMA of chunk ci + 1 (its table entry is a scalar load the compiler waits for with
         // lgkmcnt(0), so it is read before the fragment reads are issued). Unspread: every piece
         // now, before the first weight tiles; spread: one piece per kPiecesMax-th of the output
@@ -688,7 +675,7 @@ __device__ __forceinline__ void k16_pass_step(const K16Args& a, int ks, int& ci,
         const bool last = kk == KC - 1 || (FULL ? S == 7 : S + 1 == ks);
         constexpr bool whole_next = LNERF_K16_FULLDMA && FULL && S / KC + 1 < 8 / KC &&
                                     KC * NTO * PL == kPiecesMax * NW && LNERF_K16_SPREAD && !Ring<PL, NW>::stagger;
-        constexpr int fd = !whole_next ? 0 : !(LNERF_K16_SPREAD2 && KC == 2) ? (kk == 0 ? 3 : 0) : kk + 1;
+        constexpr int fd = whole_next && kk == 0 ? 3 : 0;
         // the source of the chunk after this one (S / KC + 1 of the pass), for FDSRC
         const unsigned short* fdsrc = pbase + (size_t)(S / KC + 1) * (KC * NTO * PL * 512);
         k16_step<NTO, PL, NW, fd, A24>(a, FULL ? 8 : ks, S, kk, last, ci, ring, bias_ring, in, out, slab, ex, bh,
@@ -1227,8 +1214,7 @@ unsigned k16_build_knobs() {
            (LNERF_K16_PRIO != 0 ? kKnobK16Prio : 0u) | (LNERF_K16_SPREAD != 1 ? kKnobK16Spread : 0u) |
            (LNERF_PROF != 0 ? kKnobProf : 0u) | (LNERF_A24 != 1 ? kKnobA24 : 0u) |
            (LNERF_K16_PIN != 2 ? kKnobK16Pin : 0u) | (LNERF_K16_FDSRC != 1 ? kKnobK16FdSrc : 0u) |
-           (LNERF_K16_SPREAD2 != 0 ? kKnobK16Spread2 : 0u) | (LNERF_K16_ONECHUNK != 0 ? kKnobK16OneChunk : 0u) |
-           (LNERF_K16_WAVECOMP != 0 ? kKnobK16WaveComp : 0u) |
+           (LNERF_K16_ONECHUNK != 1 ? kKnobK16OneChunk : 0u) | (LNERF_K16_WAVECOMP != 1 ? kKnobK16WaveComp : 0u) |
            (LNERF_PE_DOUBLING != 1 ? kKnobPeDoubling : 0u)
 #ifdef LNERF_K16_ONLY_16_2
            | kKnobK16Only

@@ -273,10 +273,13 @@ __device__ __forceinline__ fx4 round_values(const Loads& L, int i) {
         if (i >= 2) return L.v[i];
         fx4 v = decode_a24(L.v[i]);
         const bool marked = (int)(signed char)(L.e & 0xFFu) == kSexpNonFinite;
-        if (__builtin_amdgcn_ballot_w64(marked)) {
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(marked) != 0, 0)) {
 #pragma unroll
             for (int j = 0; j < 4; ++j)
                 if (marked && __builtin_fabsf(v[j]) >= 4194304.0f) v[j] = __builtin_nanf("");
+            // a volatile statement cannot be speculated: without it the compiler if-converts this
+            // block and runs its 8 compares and selects on every half-block (~11 % of k2's VALU)
+            asm volatile("" : "+v"(v));
         }
         return v;
     }

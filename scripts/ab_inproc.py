@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--block", type=int, default=8)
     ap.add_argument("--config", default="cfg3")
+    ap.add_argument("--render", action="store_true", help="the config-5 frame (kr) instead of cfg3 training")
     a = ap.parse_args()
     import torch
     import bench
@@ -46,6 +47,8 @@ def main():
     sys.argv = [saved[0]]   # bench.py's defaults (RAYS input, Adam in the step)
     args = bench.parse()
     sys.argv = saved
+    if a.render:
+        return render_ab(a, LibEngine)
     trainers = []
     for p in a.libs:
         t = bench.Trainer(args, a.config, 0, 0, 1, None)
@@ -84,6 +87,55 @@ def main():
     print(json.dumps(out, indent=1))
     for t in trainers:
         t.close()
+
+
+def render_ab(a, LibEngine):
+    """The config-5 frame (bench.py bench_render's inputs) per library, alternating one frame each:
+    the render kernel's HIP-event time and the frame's wall time."""
+    import numpy as np
+    import torch
+    import lnerf
+    import scene
+    side, _, S, F, L, H = scene.CONFIGS["cfg5"]
+    shapes, wp, bp = scene.init_mlp(3 + 6 * F, 4, L, H)
+    mlp = lnerf.make_mlp(shapes, wp.shape[1], wp.shape[2])
+    ws = torch.from_numpy(wp).to("cuda:0")
+    bs = torch.from_numpy(bp).to("cuda:0")
+    focal = 0.5 / np.tan(0.5 * scene.CAMERA_ANGLE_X)
+    K = np.array([[focal, 0, 0.5], [0, focal, 0.5], [0, 0, 1]])
+    engs = [LibEngine(os.path.abspath(p)) for p in a.libs]
+    rays = engs[0].get_rays(side, K, scene.look_at_pose())
+    N = rays.shape[0]
+    target = torch.zeros(N, 3, dtype=torch.float32, device="cuda:0")
+    acc = torch.empty(N, 3, dtype=torch.float32, device="cuda:0")
+    loss = torch.empty(1, dtype=torch.float32, device="cuda:0")
+    res = {p: {"fused": [], "frame_ms": []} for p in a.libs}
+
+    def frame(e, timing):
+        e.render(mlp, ws, bs, rays, None, target, samples=S, input_mode=lnerf.INPUT_RAYS, num_freqs=F,
+                 flags=lnerf.FAST | lnerf.MFMA_BF16 | (lnerf.TIMING if timing else 0), acc=acc, loss=loss)
+
+    for e in engs:
+        frame(e, False)
+    torch.cuda.synchronize()
+    for r in range(a.rounds):
+        order = list(range(len(a.libs)))
+        if r % 2:
+            order.reverse()
+        for i in order:
+            e, p = engs[i], a.libs[i]
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            frame(e, True)
+            torch.cuda.synchronize()
+            res[p]["frame_ms"].append((time.perf_counter() - t0) * 1e3)
+            res[p]["fused"].append(e.timings()["fused"])
+        print(f"round {r + 1}/{a.rounds}", flush=True)
+    out = {os.path.basename(p): {k: {"median": round(statistics.median(v), 4), "mean": round(statistics.fmean(v), 4),
+                                     "n": len(v)} for k, v in res[p].items()} for p in a.libs}
+    print(json.dumps(out, indent=1))
+    for e in engs:
+        e.close()
 
 
 if __name__ == "__main__":

@@ -180,7 +180,8 @@ enum {
 
 /* Engine options (lnerf_ctx_set_option). */
 enum {
-    LNERF_OPT_DW_GRID = 1     /* dW kernel workgroups per step (16..4096; 0 = the default 512) */
+    LNERF_OPT_DW_GRID = 1     /* dW kernel workgroups per step (16..4096; 0 = the default: 512 from
+                                 65 536 sample rows up, samples / 128 below, at least 256)       */
 };
 
 /* Optional outputs (device pointers; any may be NULL). */

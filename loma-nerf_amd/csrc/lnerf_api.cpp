@@ -468,7 +468,7 @@ struct lnerf_ctx {
     hipEvent_t ev[7] = {};
     bool timed = false;
     int last_path = 0;   // lnerf_ctx_last_path
-    int dw_grid = 0;     // LNERF_OPT_DW_GRID (0: kDefaultDwGrid)
+    int dw_grid = 0;     // LNERF_OPT_DW_GRID (0: default_dw_grid)
     FusedPlan last_plan{};   // the last fused training step's plan (lnerf_ctx_relu_masks)
     bool last_k16_train = false;
 };

@@ -176,7 +176,8 @@ void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S, bool train, int
     // LNERF_OPT_DW_GRID; 512 by default) split between the layers in proportion to the slab bytes
     // each one streams (kt + nt tiles per 32-sample block): the kernel is bandwidth-bound, so
     // equal bytes per workgroup balance it. One partial per split.
-    const int grid = dw_grid > 0 ? (dw_grid < 16 ? 16 : dw_grid > 4096 ? 4096 : dw_grid) : kDefaultDwGrid;
+    const int grid = dw_grid > 0 ? (dw_grid < 16 ? 16 : dw_grid > 4096 ? 4096 : dw_grid)
+                                 : default_dw_grid((long long)rays * S);
     // (the head weighted for its bf16x6 split under fp16x3, LNERF_DW16_HEAD_WEIGHT; every precision
     // shares the layout so that the workspace size does not depend on it)
     const int hw = LNERF_DW16_HEADX6 ? LNERF_DW16_HEAD_WEIGHT : 1;

@@ -13,6 +13,13 @@ namespace lnerf {
 constexpr int kWmaxParts = 32;   // blocks per layer of the max|W| pass before the fp16x3 packing
 constexpr int kHeadCols = 16;    // head columns with their own fp16x3 weight shift (k16 head outputs)
 constexpr int kDefaultDwGrid = 512;   // dW workgroups per step unless LNERF_OPT_DW_GRID says otherwise
+// The default budget for a batch of `samples` sample rows: 512 at the bench size and above, down to
+// 256 for smaller batches, where k2 is latency-bound and its time flat from 256 to 512 workgroups
+// while the in-order reduce over the splits grows with them (config 2, 32 768 samples, round 5:
+// 256 -> 0.073 ms per step, 512 -> 0.082; cfg3 keeps 512: 384 -> 0.88 ms of k2, 512 -> 0.73)
+__host__ __device__ constexpr int default_dw_grid(long long samples) {
+    return samples / 128 >= kDefaultDwGrid ? kDefaultDwGrid : samples / 128 <= 256 ? 256 : (int)(samples / 128);
+}
 // fp16x3 training runs the head's dW on the bf16x6 split (lnerf_dw16.hip kHeadX6), twice the
 // MFMAs and a heavier split per sample: the head gets LNERF_DW16_HEAD_WEIGHT x its byte share of
 // the dW workgroups (make_layout), so its splits do not finish last
@@ -220,7 +227,7 @@ struct FusedPlan {
 bool fused_supported(const lnerf_mlp& mlp, int rays, int S, int input_mode, const char** why,
                      bool head_fit = false);
 // train = false sizes the forward-only (render) workspace: packed weights + loss partials.
-// dw_grid: the dW kernel's workgroup budget (0 = kDefaultDwGrid; LNERF_OPT_DW_GRID).
+// dw_grid: the dW kernel's workgroup budget (0 = default_dw_grid; LNERF_OPT_DW_GRID).
 size_t fused_workspace_bytes(const lnerf_mlp& mlp, int rays, int S, bool train = true, int dw_grid = 0);
 // flags select the MFMA precision and the workgroup shape (LNERF_MFMA_*, LNERF_K16_W4; lnerf.h)
 void fused_plan(FusedPlan& p, const lnerf_mlp& mlp, const lnerf_batch& b, void* ws_base, int flags,

@@ -382,6 +382,11 @@ template <int NTO, int PL, int NW>
 constexpr int pass_kc() {
     return (LNERF_K16_ONECHUNK && NTO == 1) ? 8 : Ring<PL, NW>::KC;
 }
+// EPIFMA: the forward epilogue's unscale and bias as one fma (round 5, in-process A/B: k1
+// 1.279 -> 1.261 ms; round 4's bench-level A/B had called it neutral)
+#ifndef LNERF_K16_EPIFMA
+#define LNERF_K16_EPIFMA 1
+#endif
 // WAVECOMP: the compositing's along-ray scans in-wave (comp::composite_tile_wave: 4 workgroup
 // barriers instead of 3 log2 S + 4; round 5: k1 -0.2 %, with ONECHUNK -1.1 %)
 #ifndef LNERF_K16_WAVECOMP
@@ -949,11 +954,17 @@ k16_fwd_bwd_kernel(K16Args a) {
             bias_read<HT>(std::make_integer_sequence<int, HT>{}, bl, bv);
             // values in descending bit order (feature 4o + i ends in bit 4o + i of lo / hi)
             unsigned mlo = 0u, mhi = 0u;
+            // EPIFMA: unscale and bias as one fma (the scale is a power of two, so out 2^sh is exact
+            // and the sum rounds once either way; only a subnormal out 2^sh would differ, in fma's
+            // favour)
+            const float shs = __builtin_ldexpf(1.0f, sh);
 #pragma unroll
             for (int o = HT - 1; o >= 0; --o) {
 #pragma unroll
                 for (int i = 3; i >= 0; --i) {
-                    const float v = (PL >= 2 ? __builtin_ldexpf(out[o][i], sh) : out[o][i]) + bv[o][i];
+                    const float v = LNERF_K16_EPIFMA && PL >= 2
+                                        ? __builtin_fmaf(out[o][i], shs, bv[o][i])
+                                        : (PL >= 2 ? __builtin_ldexpf(out[o][i], sh) : out[o][i]) + bv[o][i];
                     act[o][i] = relu_bit(v, o >= 8 ? mhi : mlo);
                 }
             }
@@ -1215,6 +1226,7 @@ unsigned k16_build_knobs() {
            (LNERF_PROF != 0 ? kKnobProf : 0u) | (LNERF_A24 != 1 ? kKnobA24 : 0u) |
            (LNERF_K16_PIN != 2 ? kKnobK16Pin : 0u) | (LNERF_K16_FDSRC != 1 ? kKnobK16FdSrc : 0u) |
            (LNERF_K16_ONECHUNK != 1 ? kKnobK16OneChunk : 0u) | (LNERF_K16_WAVECOMP != 1 ? kKnobK16WaveComp : 0u) |
+           (LNERF_K16_EPIFMA != 1 ? kKnobK16EpiFma : 0u) |
            (LNERF_PE_DOUBLING != 1 ? kKnobPeDoubling : 0u)
 #ifdef LNERF_K16_ONLY_16_2
            | kKnobK16Only

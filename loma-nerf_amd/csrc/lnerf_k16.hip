@@ -280,20 +280,6 @@ __device__ __forceinline__ void store_slab_step(float* __restrict__ dst, const f
     __builtin_nontemporal_store(t0, (fx4*)(dst + n * 16 + 4 * g));
     __builtin_nontemporal_store(t1, (fx4*)(dst + 256 + n * 16 + 4 * g));
 }
-// TAILCACHED: the G_0 slab at the kernel's tail (every CU stores its 128 KiB at the same moment)
-// with the default cache policy instead of nontemporal, so the burst can land in the L2 / MALL
-#ifndef LNERF_K16_TAILCACHED
-#define LNERF_K16_TAILCACHED 0
-#endif
-__device__ __forceinline__ void store_slab_step_tail(float* __restrict__ dst, const fx4& t0, const fx4& t1) {
-    if (!LNERF_K16_TAILCACHED) {
-        store_slab_step(dst, t0, t1);
-        return;
-    }
-    const int lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
-    *(fx4*)(dst + n * 16 + 4 * g) = t0;
-    *(fx4*)(dst + 256 + n * 16 + 4 * g) = t1;
-}
 
 // The same k-step store for an int24 activation slab (lnerf_internal.h a24_slabs): the 8 values
 // as y = x 2^(ex + 8) + 1.5 2^23 (round-to-nearest integer q in the mantissa field, |q| < 2^22;
@@ -1088,7 +1074,7 @@ k16_fwd_bwd_kernel(K16Args a) {
         store_emin(a, 0, exa.get(0), store_sexp(a, 0, 1, sample_max<false>(act)));
 #pragma unroll
         for (int s = 0; s < 8; ++s)
-            if (s < a.ks_b[0]) store_slab_step_tail(g0 + s * 1024, act[2 * s], act[2 * s + 1]);
+            if (s < a.ks_b[0]) store_slab_step(g0 + s * 1024, act[2 * s], act[2 * s + 1]);
     }
 #if LNERF_PROF
     PROF_ADD(kPfTail, t_t);
@@ -1240,7 +1226,7 @@ unsigned k16_build_knobs() {
            (LNERF_PROF != 0 ? kKnobProf : 0u) | (LNERF_A24 != 1 ? kKnobA24 : 0u) |
            (LNERF_K16_PIN != 2 ? kKnobK16Pin : 0u) | (LNERF_K16_FDSRC != 1 ? kKnobK16FdSrc : 0u) |
            (LNERF_K16_ONECHUNK != 1 ? kKnobK16OneChunk : 0u) | (LNERF_K16_WAVECOMP != 1 ? kKnobK16WaveComp : 0u) |
-           (LNERF_K16_EPIFMA != 1 ? kKnobK16EpiFma : 0u) | (LNERF_K16_TAILCACHED != 0 ? kKnobK16TailCached : 0u) |
+           (LNERF_K16_EPIFMA != 1 ? kKnobK16EpiFma : 0u) |
            (LNERF_PE_DOUBLING != 1 ? kKnobPeDoubling : 0u)
 #ifdef LNERF_K16_ONLY_16_2
            | kKnobK16Only

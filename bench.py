@@ -510,23 +510,63 @@ def free_port() -> int:
     return port
 
 
-def launch_ranks(n, argv, cmd=None, env=None) -> int:
+def launch_ranks(n, argv, cmd=None, env=None, grace_s=10.0, poll_s=0.05) -> int:
     """`bench.py --gpus N` outside torchrun: start N rank processes of this same command (one per
     GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set per child, rendezvous on
-    127.0.0.1) and wait for all of them. Called before anything touches the GPU (this process never
-    initialises HIP; the ranks are children, nothing is exec'd). Rank 0 prints the JSON line.
-    Returns the first non-zero exit status (a rank that fails makes the launch fail), else 0."""
+    127.0.0.1). Called before anything touches the GPU (this process never initialises HIP; the
+    ranks are children, nothing is exec'd). Rank 0 prints the JSON line.
+
+    Fail fast: the children are polled together, and the first one that exits non-zero makes the
+    launcher terminate the rest (SIGTERM, then SIGKILL after `grace_s`) and return that status --
+    a surviving rank would otherwise sit in an RCCL collective until the process-group timeout,
+    longer than the driver's limit. SIGINT / SIGTERM sent to the launcher are
+    forwarded to every rank. Returns 0 when every rank exits 0."""
+    import signal
     import subprocess
+    import time
     cmd = cmd or [sys.executable, os.path.abspath(__file__)]
     base = dict(os.environ if env is None else env)
     base.setdefault("MASTER_ADDR", "127.0.0.1")
     base.setdefault("MASTER_PORT", str(free_port()))
     procs = []
-    for r in range(n):
-        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n))
-        procs.append(subprocess.Popen(cmd + list(argv), env=e))
-    rcs = [p.wait() for p in procs]
-    return next((rc for rc in rcs if rc != 0), 0)
+
+    def stop_all(sig=signal.SIGTERM):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    p.send_signal(sig)
+                except ProcessLookupError:
+                    pass
+        deadline = time.monotonic() + grace_s
+        for p in procs:
+            left = deadline - time.monotonic()
+            try:
+                p.wait(timeout=max(left, 0.01))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
+    def forward(signum, _frame):
+        stop_all(signal.SIGTERM)
+        raise SystemExit(128 + signum)
+
+    old = {s: signal.signal(s, forward) for s in (signal.SIGINT, signal.SIGTERM)}
+    try:
+        for r in range(n):
+            e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n))
+            procs.append(subprocess.Popen(cmd + list(argv), env=e))
+        while True:
+            rcs = [p.poll() for p in procs]
+            bad = next((rc for rc in rcs if rc is not None and rc != 0), None)
+            if bad is not None:
+                stop_all()
+                return bad
+            if all(rc == 0 for rc in rcs):
+                return 0
+            time.sleep(poll_s)
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
 
 
 def variant_flags(args) -> list:
@@ -571,7 +611,11 @@ def main():
     # N>1 code path can be rehearsed on a single GPU
     if world > 1 or "WORLD_SIZE" in os.environ:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        import datetime
+        # a bounded rendezvous / collective wait: a dead peer ends this rank in minutes, not after the
+        # 10-minute default, and launch_ranks then takes the whole launch down with it
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"),
+                                timeout=datetime.timedelta(seconds=int(os.environ.get("LNERF_PG_TIMEOUT_S", "180"))))
     if args.render:
         rec = bench_render(args, world, rank, local, dist)
         if rec:

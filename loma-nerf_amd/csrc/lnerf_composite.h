@@ -27,8 +27,11 @@ __device__ __forceinline__ double sample_coord(const A& a, int gs, int c) {
 // row (block-major: x, then sin and cos of 2^q x for q < F). LNERF_PE_DOUBLING: one float64 sincos
 // per coordinate, the higher frequencies by the double-angle identities in float64
 // (sin 2y = 2 sin y cos y, cos 2y = (cos y - sin y)(cos y + sin y)); after q doublings the error
-// is <= ~2^(q+1) float64 ulps, far below float32's rounding (CPU-measured at F = 10 on 5e6
-// coordinates: the rounded float32 values differ from per-frequency sin/cos in <= 7 of 5e6).
+// is ABSOLUTE, <= ~2^(q+1) float64 ulps of 1 (2^-43 at F = 10; the cos step cancels where cos 2y ~ 0,
+// so a value near a zero of sin / cos can be many float32 ulps of itself off, never more than that
+// absolute bound, ~2^-19 of float32's resolution of the unit-scale features; on random coordinates
+// the rounded float32 values differ from per-frequency sin/cos in <= 7 of 5e6, by one ulp:
+// tests/test_pe_doubling.py).
 // Otherwise one sincos per frequency, as numpy evaluates it.
 #ifndef LNERF_PE_DOUBLING
 #define LNERF_PE_DOUBLING 1
@@ -311,6 +314,7 @@ __device__ __forceinline__ void composite_fwd_wave(const A& a, int wg, float* co
 template <int TS, class A>
 __device__ __forceinline__ void composite_tile_wave(const A& a, int wg, float* comp, float* rayloss, bool grad) {
     static_assert(TS % 64 == 0, "whole waves of samples");
+    static_assert((TS / 64) * 8 <= TS, "the wave partials [TS / 64][8] fit their TS-float region at 8 TS");
     const int tid = threadIdx.x, S = a.S, lane = tid & 63, wv = tid >> 6;
     float* c_z = comp;
     float* c_gz = comp + 4 * TS;
@@ -428,7 +432,10 @@ __device__ __forceinline__ void composite_tile_wave(const A& a, int wg, float* c
         pub[wv * 8 + 5] = gb;
     }
     __syncthreads();
-    const int we = (ls - j + S - 1) >> 6;      // the wave holding the ray's last sample
+    // the wave holding the ray's last sample; a pseudo-ray past the tile's last whole ray (ls >=
+    // ntile, never valid) may end past the last wave: clamped, so the carry never reads past pub's
+    // [TS / 64][8] partials
+    const int we = min((ls - j + S - 1) >> 6, TS / 64 - 1);
     if (act && we > wv) {
         float gn = 0.0f;
         for (int w = we; w > wv; --w) gn = pub[w * 8 + 4] + pub[w * 8 + 5] * gn;

@@ -207,6 +207,7 @@ struct FusedPlan {
     size_t dbp_off[kMaxLayers];
     int dw_grid;
     float* loss_total; // device scalar
+    float* loss_stage; // the render loss's stage-1 block sums (loss_stage1_kernel)
     // k16 weight stream (lnerf_k16.hip): 16x16x32 MFMA, two waves per SIMD
     int ht16;                            // 16-wide hidden output tiles (1/2/4/8/16)
     int ks16_f[kMaxLayers], ks16_b[kMaxLayers];   // k-steps (32 features) per pass

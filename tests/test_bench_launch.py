@@ -69,3 +69,30 @@ def test_variant_labels():
                            config="cfg3")
     if not os.environ.get("LNERF_LIB"):
         assert bench.variant_flags(a) == []
+
+
+BLOCKER = textwrap.dedent("""
+    import os, sys, time, datetime
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=600))
+    if dist.get_rank() == 1:
+        sys.exit(5)                      # a rank that dies after the rendezvous
+    t = torch.ones(1)
+    dist.all_reduce(t)                   # rank 0 blocks here: its peer is gone
+    time.sleep(600)
+""")
+
+
+def test_launch_ranks_fails_fast_when_a_peer_dies(tmp_path):
+    """rank 1 exits non-zero while rank 0 blocks in all_reduce; the launcher must
+    return rank 1's status within ~30 s (it terminates rank 0) instead of waiting for rank 0."""
+    import time
+    script = tmp_path / "block.py"
+    script.write_text(BLOCKER)
+    t0 = time.monotonic()
+    rc = bench.launch_ranks(2, [], cmd=[sys.executable, str(script)], grace_s=5.0,
+                            env={k: v for k, v in os.environ.items() if k not in ("MASTER_PORT", "WORLD_SIZE")})
+    took = time.monotonic() - t0
+    assert rc == 5
+    assert took < 30.0, took

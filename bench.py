@@ -635,6 +635,13 @@ def main():
     dw_flops = scene.dw_kernel_flops(shapes) * N * S
     step_flops = scene.step_flops(shapes) * N * S
     last_path = None if args.generic else t.eng.last_path()
+    # the last step's exceptional rows (lnerf_ctx_exceptional_rows; after the timed region)
+    xrows = None
+    if not args.generic and last_path and last_path.get("planes") == 2:
+        n_x, n_last = t.eng.exceptional_rows(split=True)
+        xrows = {"rows": n_x, "of_them_last_samples": n_last, "of": len(shapes) * N * S,
+                 "note": "rows (summed over layers) that dw16 multiplied on the bf16x6 split instead of "
+                         "the fp16x3 one (lnerf_internal.h kXrowD0); measured on the last step"}
     t.close()
 
     variants = variant_flags(args)
@@ -689,6 +696,8 @@ def main():
                 attach_counters(roof, k1, "cfg3", out["lib_sha16"], work=fused_flops)
             out["roofline"] = roof
             out["kernels_ms"] = kt
+            if xrows is not None:
+                out["exceptional_rows"] = xrows
             out["dw_kernel_tflops"] = dw_flops / (kt["dw"] / 1e3) / 1e12
             out["dw_kernel_frac"] = out["dw_kernel_tflops"] / peak
             # k2 streams the slabs k1 wrote: algorithmic bytes = every slab value read once

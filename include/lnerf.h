@@ -254,6 +254,14 @@ int lnerf_ctx_last_path(lnerf_ctx* ctx);
  * positive. Valid until the next call on `ctx`; an error after any other kind of call. */
 int lnerf_ctx_relu_masks(lnerf_ctx* ctx, unsigned char* out, size_t out_bytes, void* stream);
 
+/* The exceptional rows of the last training step on `ctx` (k16 + dw16 with the fp16x3 split): the
+ * sample rows, summed over the layers, that dw16 multiplied on the bf16x6 split instead of the
+ * fp16x3 one because fp16's range at their balanced shift could not keep every nonzero element to
+ * 2^-17 (every ray's last sample always is one; lnerf_internal.h kXrowT); *last_samples (nullable)
+ * receives how many of them were rays' last samples. 0 for the other precisions. Synchronises the
+ * device. An extension (no loma counterpart). */
+int lnerf_ctx_exceptional_rows(lnerf_ctx* ctx, long long* rows, long long* last_samples);
+
 /* Sets an engine option (LNERF_OPT_*) for later steps on `ctx`. Returns 0, or a negative code for
  * an unknown option or an out-of-range value. */
 int lnerf_ctx_set_option(lnerf_ctx* ctx, int option, int value);

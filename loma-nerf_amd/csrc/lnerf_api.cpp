@@ -800,6 +800,29 @@ extern "C" int lnerf_ctx_relu_masks(lnerf_ctx* ctx, unsigned char* out, size_t o
     });
 }
 
+extern "C" int lnerf_ctx_exceptional_rows(lnerf_ctx* ctx, long long* rows, long long* last_samples) {
+    return guard_int([&]() {
+        if (!ctx || !rows) fail("null argument");
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        if (!ctx->last_k16_train) fail("no k16 training step has run on this context since the last other call");
+        const FusedPlan& p = ctx->last_plan;
+        *rows = 0;
+        if (last_samples) *last_samples = 0;
+        if (p.x6 != 2) return;   // only the fp16x3 split has exceptional rows
+        HIP_OK(hipSetDevice(ctx->device));
+        std::vector<int> c((size_t)2 * p.dw_grid);
+        HIP_OK(hipDeviceSynchronize());
+        HIP_OK(hipMemcpy(c.data(), p.xcount, c.size() * sizeof(int), hipMemcpyDeviceToHost));
+        long long t = 0, l = 0;
+        for (int i = 0; i < p.dw_grid; ++i) {
+            t += c[2 * i];
+            l += c[2 * i + 1];
+        }
+        *rows = t;
+        if (last_samples) *last_samples = l;
+    });
+}
+
 extern "C" int lnerf_ctx_set_option(lnerf_ctx* ctx, int option, int value) {
     return guard_int([&]() {
         if (!ctx) fail("null ctx");

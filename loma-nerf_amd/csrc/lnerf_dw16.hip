@@ -18,7 +18,11 @@
 //    (feature l & 31, samples 8 (l >> 5) ..+7) takes two 4-sample x 16-feature blocks;
 //  * each wave owns a TI x TJ block of 32 x 32 output tiles (2 x 4 for the hidden layers);
 //  * db from the same registers (per-feature partial sums, reduced in LDS at the end);
-//  * partials per split, summed in order by grad_reduce_kernel (deterministic, no atomics).
+//  * partials per split, summed in order by grad_reduce_kernel (deterministic, no atomics);
+//  * under fp16x3, the exceptional rows of the split's range (lnerf_internal.h kXrowD0: rows far
+//    below or above the layer's product scale, every ray's last sample) are dropped from the fp16x3
+//    products and multiplied afterwards on the bf16x6 split, gathered 16 to a group, into the same
+//    accumulators (xrow_pass).
 #include "lnerf_internal.h"
 
 namespace lnerf {
@@ -41,6 +45,11 @@ typedef _Float16 hf4 __attribute__((ext_vector_type(4)));
 #define LNERF_DW16_DEPTH 3
 #endif
 
+// XROW: the exceptional-row pass under fp16x3 (A/B: 0 = round 5's plain balanced split for every row)
+#ifndef LNERF_DW16_XROW
+#define LNERF_DW16_XROW 1
+#endif
+
 constexpr int kThreads = 512;
 constexpr int kRows = 512;                  // A rows [0, 256) and G rows [256, 512) of the image
 // one plane of a half-block: [16 samples][512 features] 16-bit, each sample's row padded by 64 B
@@ -55,13 +64,13 @@ constexpr int kImgRow = kRows * 2 + (LNERF_DW16_SWZ ? 0 : 64);
 __host__ __device__ constexpr int swz(int row) { return LNERF_DW16_SWZ ? (0x18140C00 >> (8 * (row & 3))) & 0xFF : 0; }
 constexpr int kPlaneBytes = 16 * kImgRow;
 // PL: the split of a dW launch -- 3 = bf16x6, 2 = fp16x3, 1 = bf16 (all x 2^e, per-sample shifts)
-// -- and kHeadX6 = 4: the bf16x6 split on an fp16x3 training's int24 activation slabs, the HEAD
-// layer's dW under fp16x3 (LNERF_DW16_HEADX6): bf16 planes keep fp32's exponent range, so a head G
-// row whose sigma gradient sits 2^30 above its rgb gradients (a tiny sigma behind the delta = 1e8
-// of train_nerf.py:306-311) loses no rgb column to fp16's subnormals
-constexpr int kHeadX6 = 4;
-__host__ __device__ constexpr int nplanes(int PL) { return PL == kHeadX6 ? 3 : PL; }
-__host__ __device__ constexpr bool a24k(int PL) { return PL == kHeadX6 || a24_slabs(PL); }
+// -- and kX6A24 = 4: the bf16x6 split of an fp16x3 training's int24 activation slabs, which the
+// exceptional rows take (xrow_pass): bf16 planes keep fp32's exponent range
+constexpr int kX6A24 = 4;
+__host__ __device__ constexpr int nplanes(int PL) { return PL == kX6A24 ? 3 : PL; }
+__host__ __device__ constexpr bool a24k(int PL) { return PL == kX6A24 || a24_slabs(PL); }
+// the split of the exceptional rows under fp16x3 training
+constexpr int kXrowPL = a24_slabs(2) ? kX6A24 : 3;
 template <int PL>
 constexpr int image_bytes() { return nplanes(PL) * kPlaneBytes; }
 
@@ -80,7 +89,8 @@ struct Dw16Args {
     size_t dwp_off[kMaxLayers];
     float* db_part;
     size_t dbp_off[kMaxLayers];
-    const unsigned short* sexp; // k1's per-sample shifts [l][position]: byte 0 A_{l-1}, byte 1 G_l
+    const unsigned* sexp;       // k1's per-sample words [l][position] (sexp_xa / sexp_xg / sexp_dmax)
+    int* xcount;                // per workgroup: the exceptional rows it multiplied, of them last samples
     int rpad;                   // slab positions per layer
     const int* eshift;          // per-layer product shift E_l (k1_reduce_kernel)
     int L;
@@ -127,7 +137,7 @@ __device__ __forceinline__ int image_row(int i, const RowMap& m) {
 
 struct Loads {
     fx4 v[4];
-    unsigned e;   // the sample's k1 shifts: byte 0 its A row's, byte 1 its G row's (int8)
+    unsigned e;   // the sample's k1 word (sexp_xa, sexp_xg, sexp_dmax)
 };
 
 // Per-sample balancing of the split: the product of a sample's A row and G row is what dW sums,
@@ -141,7 +151,7 @@ struct Loads {
 // infinity (k1 store_sexp, encoded at shift 0): its G row keeps its own shift and the A row takes
 // the rest of E, so the product scale stays 2^E; its terms are non-finite anyway.
 __device__ __forceinline__ void sample_shifts(unsigned e, int E, int& ea, int& eg) {
-    const int xa = (int)(signed char)(e & 0xFFu), xg = (int)(signed char)(e >> 8);
+    const int xa = sexp_xa(e), xg = sexp_xg(e);
     if (xa == -128 || xg == -128) {
         ea = xa < -126 ? 0 : xa;
         eg = xg == -128 ? 0 : xg;
@@ -161,7 +171,7 @@ __device__ __forceinline__ void sample_shifts(unsigned e, int E, int& ea, int& e
 // its use): rows past the layer's tiles are never split, half-blocks past the split land in the
 // idle image and add nothing to db (the callers' hb < hb1 guards).
 template <bool A24>
-__device__ __forceinline__ void issue_loads(const float* A, const float* G, const unsigned short* se, int kt,
+__device__ __forceinline__ void issue_loads(const float* A, const float* G, const unsigned* se, int kt,
                                             int nt, const RowMap& m, int hb, int hb_end, Loads& L) {
     const bool in = hb < hb_end;
     const int hbc = in ? hb : max(0, hb_end - 1);
@@ -252,16 +262,32 @@ __device__ __forceinline__ void write_planes_row(const fx4& v, int i, unsigned c
 // the split scales 2^ea (A rows) and 2^eg (G rows) of a half-block's sample (sample_shifts); with
 // int24 A slabs the A values arrive as q = x 2^(xa + 8), so their scale is 2^(ea - xa - 8) (1 for an
 // all-zero row, whose q are 0)
+// An exceptional row (lnerf_internal.h kXrowD0): a live row (neither all-zero, -128, nor a non-finite
+// activation row, kSexpNonFinite) whose deficit d = xa + xg - E_l is negative (products above the
+// layer's scale: a ray's last sample, which k1 keeps out of E_l) or above the row's dmax (kXrowD0;
+// kXrowLast = 127 for every ray's last sample: exceptional only above the scale)
+__device__ __forceinline__ bool xrow(unsigned e, int E) {
+    const int xa = sexp_xa(e), xg = sexp_xg(e);
+    const int d = xa + xg - E;
+    return xa > -127 && xg > -127 && (d < 0 || d > sexp_dmax(e));
+}
+
 template <int PL>
 __device__ __forceinline__ void sample_scales(unsigned e, int E, float& sa, float& sg) {
     int ea, eg;
     sample_shifts(e, E, ea, eg);
     if constexpr (a24k(PL)) {
-        const int xa = (int)(signed char)(e & 0xFFu);
+        const int xa = sexp_xa(e);
         ea = xa == -128 ? 0 : ea - (xa == kSexpNonFinite ? 0 : xa) - 8;
     }
     sa = __builtin_ldexpf(1.0f, ea);
     sg = __builtin_ldexpf(1.0f, eg);
+    if constexpr (PL == 2 && LNERF_DW16_XROW) {
+        // the fp16x3 products skip the exceptional rows (xrow_pass multiplies them)
+        const bool x = xrow(e, E);
+        sa = x ? 0.0f : sa;
+        sg = x ? 0.0f : sg;
+    }
 }
 
 // round i's values as the split takes them (int24 A rounds decoded). A row k1 marked non-finite
@@ -272,7 +298,7 @@ __device__ __forceinline__ fx4 round_values(const Loads& L, int i) {
     if constexpr (a24k(PL)) {
         if (i >= 2) return L.v[i];
         fx4 v = decode_a24(L.v[i]);
-        const bool marked = (int)(signed char)(L.e & 0xFFu) == kSexpNonFinite;
+        const bool marked = sexp_xa(L.e) == kSexpNonFinite;
         if (__builtin_expect(__builtin_amdgcn_ballot_w64(marked) != 0, 0)) {
 #pragma unroll
             for (int j = 0; j < 4; ++j)
@@ -327,6 +353,27 @@ __device__ __forceinline__ int frag_off(int f0) {
     return row * kImgRow + 8 * (quad ^ swz(row));
 }
 
+// One 32 x 32 output tile's products of a half-block: A fragment planes ap, G fragment planes gp
+// (small terms first)
+template <int PL>
+__device__ __forceinline__ fx16 mma_tile(const bf8 (&ap)[nplanes(PL)], const bf8 (&gp)[nplanes(PL)], fx16 c) {
+    if constexpr (PL == 2) {
+        c = mfma32h(ap[0], gp[1], c);
+        c = mfma32h(ap[1], gp[0], c);
+        c = mfma32h(ap[0], gp[0], c);
+    } else if constexpr (PL == 1) {
+        c = mfma32(ap[0], gp[0], c);
+    } else {
+        c = mfma32(ap[0], gp[2], c);
+        c = mfma32(ap[1], gp[1], c);
+        c = mfma32(ap[2], gp[0], c);
+        c = mfma32(ap[1], gp[0], c);
+        c = mfma32(ap[0], gp[1], c);
+        c = mfma32(ap[0], gp[0], c);
+    }
+    return c;
+}
+
 // The wave's TI x TJ tile block (TI 32-row tiles of A, TJ of G) on one half-block image, with
 // the split of the next half-block interleaved (round k beside output column tile k), so the
 // VALU split issues under the MFMAs. Branch-free (ACTIVE is a template parameter; past the
@@ -360,24 +407,7 @@ __device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int 
 #pragma unroll
                 for (int p = 0; p < NP; ++p) gp[p] = read_frag((unsigned char*)fl + p * kPlaneBytes + frag_off(256 + g0 + 32 * j));
 #pragma unroll
-                for (int i = 0; i < TI; ++i) {
-                    fx16 c = acc[i][j];
-                    if constexpr (PL == 2) {
-                        c = mfma32h(ap[i][0], gp[1], c);   // small terms first
-                        c = mfma32h(ap[i][1], gp[0], c);
-                        c = mfma32h(ap[i][0], gp[0], c);
-                    } else if constexpr (PL == 1) {
-                        c = mfma32(ap[i][0], gp[0], c);
-                    } else {
-                        c = mfma32(ap[i][0], gp[2], c);   // small terms first
-                        c = mfma32(ap[i][1], gp[1], c);
-                        c = mfma32(ap[i][2], gp[0], c);
-                        c = mfma32(ap[i][1], gp[0], c);
-                        c = mfma32(ap[i][0], gp[1], c);
-                        c = mfma32(ap[i][0], gp[0], c);
-                    }
-                    acc[i][j] = c;
-                }
+                for (int i = 0; i < TI; ++i) acc[i][j] = mma_tile<PL>(ap[i], gp, acc[i][j]);
             }
         }
         if (LNERF_DW16_SPLIT_LATE && (FULL || m.ok[k])) write_planes_row<PL>(round_values<PL>(nl, k), k, nxt, sa, sg, m);
@@ -389,10 +419,10 @@ __device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int 
 // (hb - hb0) & 1, the set after I holds hb + 1 (split now into the other image), the one after
 // that hb + 2 (in flight) and set I is free: it receives hb + 3.
 template <int PL, int TI, int TJ, bool ACTIVE, bool FULL, int I>
-__device__ __forceinline__ void hb_step3(const float* A, const float* G, const unsigned short* se, int kt, int nt,
+__device__ __forceinline__ void hb_step3(const float* A, const float* G, const unsigned* se, int kt, int nt,
                                          const RowMap& m, int hb, int hb0, int hb1, int a0, int g0,
                                          fx16 (&acc)[TI][TJ], Loads& L0, Loads& L1, Loads& L2, fx4 (&dbs)[2],
-                                         unsigned char* lds, int E) {
+                                         unsigned char* lds, int E, bool& xany) {
     constexpr int kIB = image_bytes<PL>();
     Loads& fr = I == 0 ? L0 : I == 1 ? L1 : L2;
     const Loads& nx = I == 0 ? L1 : I == 1 ? L2 : L0;
@@ -403,20 +433,22 @@ __device__ __forceinline__ void hb_step3(const float* A, const float* G, const u
     }
     const int cur = (hb - hb0) & 1;
     block_mma<PL, TI, TJ, ACTIVE, FULL>(lds + cur * kIB, a0, g0, acc, nx, lds + (cur ^ 1) * kIB, m, E, hb + 1 < hb1);
+    // (after the split of hb + 1, which already waited for its k1 word)
+    if constexpr (PL == 2 && LNERF_DW16_XROW) xany |= hb + 1 < hb1 && xrow(nx.e, E);
     __syncthreads();
 }
 
 template <int PL, int TI, int TJ, bool ACTIVE, bool FULL>
-__device__ __forceinline__ void hb_loop3(const float* A, const float* G, const unsigned short* se, int kt, int nt,
+__device__ __forceinline__ void hb_loop3(const float* A, const float* G, const unsigned* se, int kt, int nt,
                                          const RowMap& m, int hb0, int hb1, int a0, int g0, fx16 (&acc)[TI][TJ],
                                          Loads& L0, Loads& L1, Loads& L2, fx4 (&dbs)[2], unsigned char* lds,
-                                         int E) {
+                                         int E, bool& xany) {
     // whole triples only (one loop body; remainder copies make the compiler spill the
     // accumulators): the steps past hb1 split zero-scaled (zero) planes and add nothing
     for (int hb = hb0; hb < hb1; hb += 3) {
-        hb_step3<PL, TI, TJ, ACTIVE, FULL, 0>(A, G, se, kt, nt, m, hb, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
-        hb_step3<PL, TI, TJ, ACTIVE, FULL, 1>(A, G, se, kt, nt, m, hb + 1, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
-        hb_step3<PL, TI, TJ, ACTIVE, FULL, 2>(A, G, se, kt, nt, m, hb + 2, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
+        hb_step3<PL, TI, TJ, ACTIVE, FULL, 0>(A, G, se, kt, nt, m, hb, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E, xany);
+        hb_step3<PL, TI, TJ, ACTIVE, FULL, 1>(A, G, se, kt, nt, m, hb + 1, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E, xany);
+        hb_step3<PL, TI, TJ, ACTIVE, FULL, 2>(A, G, se, kt, nt, m, hb + 2, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E, xany);
     }
 }
 
@@ -424,10 +456,10 @@ __device__ __forceinline__ void hb_loop3(const float* A, const float* G, const u
 // entering hb, set I held hb (split last step, free: it receives hb + 2), set I ^ 1 holds hb + 1
 // (split now). 17 fewer registers than the 3-deep rotation.
 template <int PL, int TI, int TJ, bool ACTIVE, bool FULL, int I>
-__device__ __forceinline__ void hb_step2(const float* A, const float* G, const unsigned short* se, int kt, int nt,
+__device__ __forceinline__ void hb_step2(const float* A, const float* G, const unsigned* se, int kt, int nt,
                                          const RowMap& m, int hb, int hb0, int hb1, int a0, int g0,
                                          fx16 (&acc)[TI][TJ], Loads& L0, Loads& L1, fx4 (&dbs)[2],
-                                         unsigned char* lds, int E) {
+                                         unsigned char* lds, int E, bool& xany) {
     constexpr int kIB = image_bytes<PL>();
     Loads& fr = I == 0 ? L0 : L1;
     const Loads& nx = I == 0 ? L1 : L0;
@@ -438,17 +470,168 @@ __device__ __forceinline__ void hb_step2(const float* A, const float* G, const u
     }
     const int cur = (hb - hb0) & 1;
     block_mma<PL, TI, TJ, ACTIVE, FULL>(lds + cur * kIB, a0, g0, acc, nx, lds + (cur ^ 1) * kIB, m, E, hb + 1 < hb1);
+    // (after the split of hb + 1, which already waited for its k1 word)
+    if constexpr (PL == 2 && LNERF_DW16_XROW) xany |= hb + 1 < hb1 && xrow(nx.e, E);
     __syncthreads();
 }
 
 template <int PL, int TI, int TJ, bool ACTIVE, bool FULL>
-__device__ __forceinline__ void hb_loop2(const float* A, const float* G, const unsigned short* se, int kt, int nt,
+__device__ __forceinline__ void hb_loop2(const float* A, const float* G, const unsigned* se, int kt, int nt,
                                          const RowMap& m, int hb0, int hb1, int a0, int g0, fx16 (&acc)[TI][TJ],
-                                         Loads& L0, Loads& L1, fx4 (&dbs)[2], unsigned char* lds, int E) {
+                                         Loads& L0, Loads& L1, fx4 (&dbs)[2], unsigned char* lds, int E,
+                                         bool& xany) {
     for (int hb = hb0; hb < hb1; hb += 2) {
-        hb_step2<PL, TI, TJ, ACTIVE, FULL, 0>(A, G, se, kt, nt, m, hb, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E);
-        hb_step2<PL, TI, TJ, ACTIVE, FULL, 1>(A, G, se, kt, nt, m, hb + 1, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E);
+        hb_step2<PL, TI, TJ, ACTIVE, FULL, 0>(A, G, se, kt, nt, m, hb, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E, xany);
+        hb_step2<PL, TI, TJ, ACTIVE, FULL, 1>(A, G, se, kt, nt, m, hb + 1, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E, xany);
     }
+}
+
+// ---- exceptional rows (lnerf_internal.h kXrowD0) ----------------------------------------------
+// The four rounds of loads of ONE sample row at slab position p (p < 0: position 0, whose values
+// the caller scales by 0): the thread's [h][sample][4-feature quad] offset inside the row's
+// half-block with the sample index replaced by p's.
+template <bool A24>
+__device__ __forceinline__ void gather_loads(const float* A, const float* G, const unsigned* se, int kt, int nt,
+                                             const RowMap& m, int p, Loads& L) {
+    const int pc = p < 0 ? 0 : p;
+    L.e = se[pc];
+    const int hb = pc >> 4, blk = hb >> 1, half = hb & 1;
+    const int u = ((int)threadIdx.x & 127 & ~0x3C) | ((pc & 15) << 2);
+    const float* pg = G + (size_t)blk * nt * 1024 + half * 512 + 4 * u;
+    if constexpr (A24) {
+        const unsigned char* pa = (const unsigned char*)A + ((size_t)blk * kt * 3072 + half * 1536 + 12 * u);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const unsigned* q = (const unsigned*)(pa + m.tile[i] * 3072);
+            L.v[i] = fx4{__builtin_bit_cast(float, q[0]), __builtin_bit_cast(float, q[1]),
+                         __builtin_bit_cast(float, q[2]), 0.0f};
+        }
+    } else {
+        const float* pa = A + (size_t)blk * kt * 1024 + half * 512 + 4 * u;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) L.v[i] = *(const fx4*)(pa + m.tile[i] * 1024);
+    }
+#pragma unroll
+    for (int i = 2; i < 4; ++i) L.v[i] = *(const fx4*)(pg + m.tile[i] * 1024);
+}
+
+// the wave's TI x TJ tile block of one image (no split interleaved)
+template <int PL, int TI, int TJ>
+__device__ __forceinline__ void mma_block(const unsigned char* img, int a0, int g0, fx16 (&acc)[TI][TJ]) {
+    constexpr int NP = nplanes(PL);
+    bf8 ap[TI][NP];
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) ap[i][p] = read_frag((unsigned char*)img + p * kPlaneBytes + frag_off(a0 + 32 * i));
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+        bf8 gp[NP];
+#pragma unroll
+        for (int p = 0; p < NP; ++p) gp[p] = read_frag((unsigned char*)img + p * kPlaneBytes + frag_off(256 + g0 + 32 * j));
+#pragma unroll
+        for (int i = 0; i < TI; ++i) acc[i][j] = mma_tile<PL>(ap[i], gp, acc[i][j]);
+    }
+}
+
+// After the fp16x3 half-blocks of a split: its exceptional rows -- found by a scan of its
+// positions' k1 words (the same xrow test that zeroed their scales in the main loop), listed in
+// position order into an LDS ring and multiplied 16 at a time on the bf16x6 split into the same
+// accumulators (products at the layer's scale 2^E: the per-sample balanced shifts, which bf16's
+// exponent range carries at any deficit); each group's gathered loads are issued before the
+// previous group is split. `any`: some thread's main loop met an exceptional row; a split that met
+// none (the bench batch: all but a handful) skips the scan after two barriers. Deterministic: the
+// groups follow position order. Returns the rows multiplied and, of them, rays' last samples.
+constexpr int kXrowRing = 4096;   // > 15 pending + 4 x 512 listed per scan step
+template <int TI, int TJ>
+__device__ __forceinline__ int2 xrow_pass(const float* A, const float* G, const unsigned* se, int KT, int NT,
+                                          const RowMap& m, int hb0, int hb1, int a0, int g0, bool active,
+                                          fx16 (&acc)[TI][TJ], unsigned char* lds, int E, bool any) {
+    constexpr int PX = kXrowPL;
+    int* ring = (int*)(lds + image_bytes<PX>());
+    int* wcnt = ring + kXrowRing;   // [2: rows, last samples][4 scan rounds][8 waves], then the any flags
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+    const int p0 = hb0 * 16, p1 = hb1 * 16;
+    const bool wany = __builtin_amdgcn_ballot_w64(any) != 0;
+    __syncthreads();   // every wave is done with the fp16x3 images
+    if (lane == 0) wcnt[64 + wave] = wany ? 1 : 0;
+    __syncthreads();
+    int anyw = 0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) anyw |= wcnt[64 + w];
+    if (!anyw) return int2{0, 0};
+    int head = 0, tail = 0, ntail = 0;   // workgroup-uniform (ring slot = index % kXrowRing)
+    for (int base = p0; base < p1; base += 4 * kThreads) {
+        bool f[4], tl[4];
+        unsigned long long bal[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int p = base + k * kThreads + tid;
+            const unsigned e = se[p < p1 ? p : p0];
+            f[k] = p < p1 && xrow(e, E);
+            tl[k] = f[k] && sexp_dmax(e) == kXrowLast;
+        }
+        __syncthreads();   // the previous step's counts are read
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            bal[k] = __builtin_amdgcn_ballot_w64(f[k]);
+            const unsigned long long bt = __builtin_amdgcn_ballot_w64(tl[k]);
+            if (lane == 0) {
+                wcnt[k * 8 + wave] = __builtin_popcountll(bal[k]);
+                wcnt[32 + k * 8 + wave] = __builtin_popcountll(bt);
+            }
+        }
+        __syncthreads();
+        int off = tail;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            int mine = off;
+            for (int w = 0; w < 8; ++w) {
+                const int c = wcnt[k * 8 + w];
+                mine += w < wave ? c : 0;
+                off += c;
+                ntail += wcnt[32 + k * 8 + w];
+            }
+            if (f[k]) {
+                const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(bal[k] >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((unsigned)bal[k], 0u));
+                ring[(mine + r) % kXrowRing] = base + k * kThreads + tid;
+            }
+        }
+        tail = off;
+        __syncthreads();
+        // the whole groups now in the ring (every remaining entry after the last scan step)
+        const bool last = base + 4 * kThreads >= p1;
+        const int ng = last ? (tail - head + 15) / 16 : (tail - head) / 16;
+        if (ng > 0) {
+            auto pos = [&](int gi) {
+                const int at = head + 16 * gi + m.isamp;
+                return at < tail ? ring[at % kXrowRing] : -1;
+            };
+            int pc = pos(0);
+            Loads Lc;
+            gather_loads<a24k(PX)>(A, G, se, KT, NT, m, pc, Lc);
+            for (int gi = 0; gi < ng; ++gi) {
+                const int pn = gi + 1 < ng ? pos(gi + 1) : -1;
+                Loads Ln;
+                if (gi + 1 < ng) gather_loads<a24k(PX)>(A, G, se, KT, NT, m, pn, Ln);
+                float sa, sg;
+                sample_scales<PX>(Lc.e, E, sa, sg);
+                sa = pc < 0 ? 0.0f : sa;
+                sg = pc < 0 ? 0.0f : sg;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (m.ok[i]) write_planes_row<PX>(round_values<PX>(Lc, i), i, lds, sa, sg, m);
+                __syncthreads();
+                if (active) mma_block<PX, TI, TJ>(lds, a0, g0, acc);
+                __syncthreads();
+                Lc = Ln;
+                pc = pn;
+            }
+            head = head + 16 * ng < tail ? head + 16 * ng : tail;
+        }
+    }
+    return int2{tail, ntail};
 }
 
 // One split of layer l with TI x TJ tile blocks per wave (the layer's ceil(KT/TI) x ceil(NT/TJ)
@@ -478,25 +661,28 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
     const RowMap m = row_map(KT, NT);
     // the per-sample balanced shifts (sample_shifts): every product carries 2^E, removed from the
     // partials at the end (exact)
-    const unsigned short* se = a.sexp + (size_t)l * a.rpad;
+    const unsigned* se = a.sexp + (size_t)l * a.rpad;
     const int E = a.eshift[l];
     const bool full = KT == 8 && NT == 8;
 #if LNERF_DW16_DEPTH == 2
     Loads L0, L1;
+    bool xany = false;   // this thread split an exceptional row (fp16x3: xrow_pass)
     issue_loads<a24k(PL)>(A, G, se, KT, NT, m, hb0, hb1, L0);
     issue_loads<a24k(PL)>(A, G, se, KT, NT, m, hb0 + 1, hb1, L1);
     if (hb0 < hb1) {
         dbs[0] += L0.v[2];
         dbs[1] += L0.v[3];
         write_planes<PL>(L0, lds, E, m);
+        if constexpr (PL == 2 && LNERF_DW16_XROW) xany = xrow(L0.e, E);
     }
     __syncthreads();
-    if (active && full) hb_loop2<PL, TI, TJ, true, true>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E);
-    else if (active) hb_loop2<PL, TI, TJ, true, false>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E);
-    else if (full) hb_loop2<PL, TI, TJ, false, true>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E);
-    else hb_loop2<PL, TI, TJ, false, false>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E);
+    if (active && full) hb_loop2<PL, TI, TJ, true, true>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E, xany);
+    else if (active) hb_loop2<PL, TI, TJ, true, false>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E, xany);
+    else if (full) hb_loop2<PL, TI, TJ, false, true>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E, xany);
+    else hb_loop2<PL, TI, TJ, false, false>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E, xany);
 #else
     Loads L0, L1, L2;
+    bool xany = false;   // this thread split an exceptional row (fp16x3: xrow_pass)
     issue_loads<a24k(PL)>(A, G, se, KT, NT, m, hb0, hb1, L0);
     issue_loads<a24k(PL)>(A, G, se, KT, NT, m, hb0 + 1, hb1, L1);
     issue_loads<a24k(PL)>(A, G, se, KT, NT, m, hb0 + 2, hb1, L2);
@@ -504,13 +690,24 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
         dbs[0] += L0.v[2];
         dbs[1] += L0.v[3];
         write_planes<PL>(L0, lds, E, m);
+        if constexpr (PL == 2 && LNERF_DW16_XROW) xany = xrow(L0.e, E);
     }
     __syncthreads();
-    if (active && full) hb_loop3<PL, TI, TJ, true, true>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
-    else if (active) hb_loop3<PL, TI, TJ, true, false>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
-    else if (full) hb_loop3<PL, TI, TJ, false, true>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
-    else hb_loop3<PL, TI, TJ, false, false>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E);
+    if (active && full) hb_loop3<PL, TI, TJ, true, true>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E, xany);
+    else if (active) hb_loop3<PL, TI, TJ, true, false>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E, xany);
+    else if (full) hb_loop3<PL, TI, TJ, false, true>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E, xany);
+    else hb_loop3<PL, TI, TJ, false, false>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, acc, L0, L1, L2, dbs, lds, E, xany);
 #endif
+
+    if constexpr (PL == 2 && LNERF_DW16_XROW) {
+        const int2 nx = xrow_pass<TI, TJ>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, active, acc, lds, E, xany);
+        if (threadIdx.x == 0) {
+            a.xcount[2 * blockIdx.x] = nx.x;
+            a.xcount[2 * blockIdx.x + 1] = nx.y;
+        }
+    } else {
+        if (threadIdx.x == 0) a.xcount[2 * blockIdx.x] = a.xcount[2 * blockIdx.x + 1] = 0;
+    }
 
     // partial [split][k][j], k < KT*32, j < NT*32 (32x32 C/D layout: row (r&3)+8(r>>2)+4h, col l&31)
     if (active) {
@@ -556,21 +753,21 @@ __host__ __device__ __forceinline__ int dw_shape(int kt, int nt) {
     return 2;
 }
 
+// LDS of a dW workgroup: the two half-block images; under fp16x3 the exceptional rows' bf16x6 image
+// and position ring (xrow_pass) reuse and extend them
+template <int PL>
+constexpr int dw_lds_bytes() {
+    constexpr int main = 2 * image_bytes<PL>();
+    constexpr int xr = PL == 2 && LNERF_DW16_XROW ? image_bytes<kXrowPL>() + (kXrowRing + 72) * 4 : 0;
+    return main > xr ? main : xr;
+}
+
 template <int PL>
 __global__ void __launch_bounds__(kThreads, 1) dw16_kernel(Dw16Args a) {
-    // fp16x3 with the head on the bf16x6 split: room for its three planes
-    constexpr bool headx6 = PL == 2 && LNERF_DW16_HEADX6 && a24_slabs(2);
-    __shared__ __attribute__((aligned(16))) unsigned char lds[2 * image_bytes<headx6 ? kHeadX6 : PL>()];
+    __shared__ __attribute__((aligned(16))) unsigned char lds[dw_lds_bytes<PL>()];
     int li = 0;
     while (li + 1 < a.nl && (int)blockIdx.x >= a.wg_off[li + 1]) ++li;
     const int l = a.lid[li], sp = blockIdx.x - a.wg_off[li];
-    if constexpr (headx6) {
-        // the head (<= 16 outputs: one 32-column tile, kt <= 8: the 1 x 1 shape)
-        if (l == a.L - 1 && dw_shape(a.kt[l], a.nt[l]) == 0) {
-            dw_split<kHeadX6, 1, 1>(a, l, sp, lds);
-            return;
-        }
-    }
     switch (dw_shape(a.kt[l], a.nt[l])) {
         case 0: dw_split<PL, 1, 1>(a, l, sp, lds); break;
         case 1: dw_split<PL, 1, 2>(a, l, sp, lds); break;
@@ -626,7 +823,7 @@ __global__ void __launch_bounds__(1024) k1_reduce_kernel(const int* __restrict__
 unsigned dw16_build_knobs() {
     return (LNERF_DW16_SPLIT_LATE != 1 ? kKnobDwSplitLate : 0u) | (LNERF_DW16_DEPTH != 3 ? kKnobDwDepth : 0u) |
            (LNERF_DW16_SWZ != 1 ? kKnobDwSwz : 0u) | (LNERF_A24 != 1 ? kKnobA24 : 0u) |
-           (LNERF_DW16_HEADX6 != 1 || LNERF_DW16_HEAD_WEIGHT != 2 ? kKnobDwHeadX6 : 0u);
+           (LNERF_DW16_XROW != 1 ? kKnobDwXrow : 0u);
 }
 
 void dw16_launch(const FusedPlan& p, hipStream_t s) {
@@ -649,7 +846,8 @@ void dw16_launch(const FusedPlan& p, hipStream_t s) {
     a.blocks = p.blocks;
     a.dw_part = p.dw_part;
     a.db_part = p.db_part;
-    a.sexp = (const unsigned short*)p.sexp;
+    a.sexp = p.sexp;
+    a.xcount = p.xcount;
     a.rpad = p.num_wg * p.tile;
     a.eshift = p.dw_shift;
     a.L = p.L;

@@ -198,10 +198,7 @@ void make_layout(Layout& y, const lnerf_mlp& m, int rays, int S, bool train, int
     // equal bytes per workgroup balance it. One partial per split.
     const int grid = dw_grid > 0 ? (dw_grid < 16 ? 16 : dw_grid > 4096 ? 4096 : dw_grid)
                                  : default_dw_grid((long long)rays * S);
-    // (the head weighted for its bf16x6 split under fp16x3, LNERF_DW16_HEAD_WEIGHT; every precision
-    // shares the layout so that the workspace size does not depend on it)
-    const int hw = LNERF_DW16_HEADX6 ? LNERF_DW16_HEAD_WEIGHT : 1;
-    auto weight = [&](int l) { return (kt[l] + nt[l]) * (l == L - 1 ? hw : 1); };
+    auto weight = [&](int l) { return kt[l] + nt[l]; };
     int tiles_sum = 0;
     for (int l = 0; l < L; ++l) tiles_sum += weight(l);
     size_t dwp = 0, dbp = 0;
@@ -254,8 +251,9 @@ static size_t workspace_floats(const lnerf_mlp& m, int rays, int S, bool train, 
            align_up(y.b16_total, 64) + align_up(y.mask_total * 2, 64) + 64 +   // + the fp16x3 shifts
            align_up((size_t)kMaxLayers * kWmaxParts + kWmaxParts * kHeadCols, 64) +   // per-block max|W|
            align_up((size_t)kHeadCols, 64) +                                     // head column max|W|
-           (train ? align_up((size_t)m.num_layers * y.num_wg * tile / 2, 64) +   // per-sample shifts
-                        align_up((size_t)m.num_layers * y.num_wg * 8, 64) : 0);     // per-wave minima
+           (train ? align_up((size_t)m.num_layers * y.num_wg * tile, 64) +      // per-sample words
+                        align_up((size_t)m.num_layers * y.num_wg * 8, 64) +         // per-wave minima
+                        align_up((size_t)2 * y.dw_grid, 64) : 0);                   // exceptional rows
 }
 
 // Either tile size (fused_plan runs 64 under LNERF_K16_W4, 128 otherwise).
@@ -329,10 +327,12 @@ static void fused_plan_tile(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch&
     p.dw_shift = p.wexp16 + kMaxLayers;
     p.wmax_part = (int*)take((size_t)kMaxLayers * kWmaxParts + kWmaxParts * kHeadCols);
     p.hexp16 = (int*)take((size_t)kHeadCols);
-    p.sexp = (signed char*)(base + off);                             // L x num_wg x tile x 2 bytes
-    if (train) off += align_up((size_t)p.L * y.num_wg * tile / 2, 64);
+    p.sexp = (unsigned*)(base + off);                                // L x num_wg x tile words
+    if (train) off += align_up((size_t)p.L * y.num_wg * tile, 64);
     p.epart = (int*)(base + off);
     if (train) off += align_up((size_t)p.L * y.num_wg * 8, 64);
+    p.xcount = (int*)(base + off);
+    if (train) off += align_up((size_t)2 * y.dw_grid, 64);
 }
 
 void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws_base, int flags, bool train,

@@ -20,15 +20,30 @@ constexpr int kDefaultDwGrid = 512;   // dW workgroups per step unless LNERF_OPT
 __host__ __device__ constexpr int default_dw_grid(long long samples) {
     return samples / 128 >= kDefaultDwGrid ? kDefaultDwGrid : samples / 128 <= 256 ? 256 : (int)(samples / 128);
 }
-// fp16x3 training runs the head's dW on the bf16x6 split (lnerf_dw16.hip kHeadX6), twice the
-// MFMAs and a heavier split per sample: the head gets LNERF_DW16_HEAD_WEIGHT x its byte share of
-// the dW workgroups (make_layout), so its splits do not finish last
-#ifndef LNERF_DW16_HEADX6
-#define LNERF_DW16_HEADX6 1
-#endif
-#ifndef LNERF_DW16_HEAD_WEIGHT
-#define LNERF_DW16_HEAD_WEIGHT 2
-#endif
+// ---- exceptional rows of the fp16x3 dW split (round 6) ------------------------------------------
+// k2 (lnerf_dw16.hip) multiplies a sample's A row and G row as fp16 hi + lo pieces at per-row
+// exponent shifts balanced around the layer's product shift E_l (the smallest xa + xg over the
+// batch, i.e. its largest products): A 2^ea, G 2^eg, ea + eg = E_l, each operand lowered by half of
+// the row's deficit d = xa + xg - E_l (sample_shifts). A row far below the layer's scale (round 5's
+// edge_finite_6x8: rows at d = 30..110, behind opaque samples and at delta = 1e8) was pushed into
+// fp16's subnormals, and lost up to ~2 % of a column made only of such rows. Round 6 multiplies
+// them exactly instead: an EXCEPTIONAL row -- d > kXrowD0 (each operand more than kXrowD0 / 2
+// binades under its own shift) or d < 0 (products above the layer's scale: a ray's last sample, the
+// delta = 1e8 row of train_nerf.py:306-311, whose sigma gradient can sit 2^45 above its rgb
+// gradients, and which therefore never sets E_l; such a row is exceptional only this way) -- is
+// dropped from the fp16x3
+// products and multiplied on the bf16x6 split (three bf16 planes per operand, fp32's exponent
+// range) into the same accumulators (xrow_pass). k1 writes each row's bound dmax (kXrowD0, or
+// kXrowLast for a last sample) beside its shifts; k2 tests d against it. Within the other rows an
+// element r binades below its row's maximum sits near 2^(13 - r - d / 2), so the balanced split
+// keeps elements down to 2^-(27 - kXrowD0 / 2) of their row's maximum in fp16's normal range.
+constexpr int kXrowD0 = 12;
+constexpr int kXrowLast = 127;   // a ray's last sample: exceptional only above the scale (d < 0)
+// k1's per-sample slab word [l][position], 4 bytes: byte 0 xa (the input row's shift), byte 2 xg (the
+// G row's), byte 3 dmax; byte 1 unused
+__host__ __device__ constexpr int sexp_xa(unsigned e) { return (int)(signed char)(e & 0xFFu); }
+__host__ __device__ constexpr int sexp_xg(unsigned e) { return (int)(signed char)((e >> 16) & 0xFFu); }
+__host__ __device__ constexpr int sexp_dmax(unsigned e) { return (int)(signed char)(e >> 24); }
 
 // ---- fp16x3 exponent shifts ------------------------------------------------------------------
 // The shift e that puts a group's largest magnitude m in [2^13, 2^14) for the fp16 hi/lo split
@@ -84,7 +99,7 @@ enum : unsigned {
     kKnobK16FullDma = 1u << 0, kKnobK16KDist = 1u << 1, kKnobK16SplitAt = 1u << 2, kKnobK16Sched = 1u << 3,
     kKnobK16Prio = 1u << 4, kKnobK16Spread = 1u << 5, kKnobProf = 1u << 6, kKnobA24 = 1u << 7,
     kKnobK16Only = 1u << 8, kKnobDwSplitLate = 1u << 9, kKnobDwDepth = 1u << 10, kKnobDwSwz = 1u << 11,
-    kKnobK16Pin = 1u << 12, kKnobK16FdSrc = 1u << 13, kKnobKrStagger = 1u << 15, kKnobDwHeadX6 = 1u << 17,
+    kKnobK16Pin = 1u << 12, kKnobK16FdSrc = 1u << 13, kKnobKrStagger = 1u << 15, kKnobDwXrow = 1u << 17,
     kKnobKrSched = 1u << 18, kKnobKrDist = 1u << 19, kKnobPeDoubling = 1u << 20, kKnobK16OneChunk = 1u << 22, kKnobK16WaveComp = 1u << 23, kKnobK16EpiFma = 1u << 24,
 };
 unsigned k16_build_knobs();
@@ -221,7 +236,9 @@ struct FusedPlan {
                                          // then the head's per-column partials [kWmaxParts][kHeadCols]
     int* hexp16;                         // x6 = 2: the head's per-column max|W| bits [kHeadCols]
     int* dw_shift;                       // per-layer dW product shift E_l (k1_reduce_kernel)
-    signed char* sexp;                   // k1's per-sample slab shifts [L][num_wg * tile][2]
+    unsigned* sexp;                      // k1's per-sample slab words [L][num_wg * tile] (sexp_xa ...)
+    int* xcount;                         // per dW workgroup: exceptional rows it multiplied, of them rays'
+                                         // last samples (xrow_pass) [dw_grid][2]
     int* epart;                          // k1's per-wave min of exA + exG [L][num_wg * waves]
 };
 

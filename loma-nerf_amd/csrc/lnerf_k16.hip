@@ -106,9 +106,10 @@ struct K16Args {
     int planes;
     const int* wexp;   // PL = 2: per-layer max|W| bits of the packed fp16 weight planes (wshift_of)
     const int* hexp;   // PL = 2: the head's per-column max|W| bits (head_col_shift)
-    // training: every sample's exponent shift of each slab row (store_sexp), [l][position][2] int8:
-    // byte 0 the input of layer l (X, A_l-1), byte 1 G_l; position = half-block * 16 + sample
-    signed char* sexp;
+    // training: every sample's word per layer (lnerf_internal.h sexp_xa / sexp_xg / sexp_dmax),
+    // [l][position] x 4 bytes: byte 0 the exponent shift of layer l's input row (X, A_l-1), byte 2
+    // G_l's, byte 3 the row's exceptional-row bound dmax; position = half-block * 16 + sample
+    unsigned char* sexp;
     int rpad;          // slab positions (num_wg * 128)
     int* epart;        // training: per-wave min over samples of exA + exG, [l][num_wg * 8]
     int head_fit;      // the mlp_fit head (comp::fit_tile) instead of the NeRF compositing
@@ -757,10 +758,11 @@ __device__ __forceinline__ float sample_max(const fx4 (&in)[kMaxT]) {
 __device__ __forceinline__ int shift_of(float m) { return fp16x3_shift(m); }
 
 // Training: this sample's exponent shift of one slab row (the shift its split used, or -128 for an
-// all-zero row), one byte per sample for dw16's per-sample balancing of A and G (lnerf_dw16.hip).
-// Issued before the pass's first DMA, so it is older than every piece a dma_barrier waits for.
-// Returns the byte.
-__device__ __forceinline__ int store_sexp(const K16Args& a, int l, int which, float m) {
+// all-zero row), for dw16's per-sample balancing of A and G (lnerf_dw16.hip). which = 0: the input
+// row of layer l (byte 0 of its word); which = 1: the G_l row, with the row's exceptional-row bound
+// dmax (bytes 2, 3). Issued before the pass's first DMA, so it is older than every piece a
+// dma_barrier waits for. Returns the shift.
+__device__ __forceinline__ int store_sexp(const K16Args& a, int l, int which, float m, int dmax = 0) {
     const int lane = threadIdx.x & 63;
     // -128: an all-zero row; -127 (activation rows only): a row with a non-finite value, int24-encoded
     // at shift 0, whose NaN / infinity codes dw16 turns back into NaN (kSexpNonFinite)
@@ -768,7 +770,9 @@ __device__ __forceinline__ int store_sexp(const K16Args& a, int l, int which, fl
     const int x = (m > 0.0f && fin) ? shift_of(m) : (which == 0 && !(m == 0.0f)) ? kSexpNonFinite : -128;
     if (lane < 16) {
         const int p = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + lane;
-        a.sexp[((size_t)l * a.rpad + p) * 2 + which] = (signed char)x;
+        unsigned char* w = a.sexp + ((size_t)l * a.rpad + p) * 4;
+        if (which == 0) *w = (unsigned char)x;
+        else *(unsigned short*)(w + 2) = (unsigned short)((x & 0xFF) | ((dmax & 0xFF) << 8));
     }
     return x;
 }
@@ -793,10 +797,11 @@ struct ExPack {
 };
 
 // Training, after layer l's G-row shift xg: the wave's min over its samples of xa + xg (rows
-// marked -128 excluded), one plain store per wave into epart[l][global wave]; k1_reduce_kernel
-// folds them into dw16's per-layer product shift E_l.
-__device__ __forceinline__ void store_emin(const K16Args& a, int l, int xa, int xg) {
-    int v = (xa < -126 || xg < -126) ? (1 << 20) : xa + xg;
+// marked -128 excluded, and every ray's last sample, which dw16 multiplies on the bf16x6 split
+// whenever its products exceed E_l: lnerf_internal.h kXrowLast), one plain store per wave into
+// epart[l][global wave]; k1_reduce_kernel folds them into dw16's per-layer product shift E_l.
+__device__ __forceinline__ void store_emin(const K16Args& a, int l, int xa, int xg, bool excluded) {
+    int v = (xa < -126 || xg < -126 || excluded) ? (1 << 20) : xa + xg;
 #pragma unroll
     for (int d = 1; d < 16; d <<= 1) v = min(v, __shfl_xor(v, d));
     if ((threadIdx.x & 63) == 0)
@@ -877,6 +882,11 @@ k16_fwd_bwd_kernel(K16Args a) {
     fx4 act[kMaxT], out[kMaxT];
     zero_tiles(act);
     ExPack exa;   // training: the forward's A-row shift of this lane's sample, per layer
+    // training: this sample is its ray's last (the delta = 1e8 row, train_nerf.py:306-311): kept out
+    // of every layer's product scale E_l and an exceptional row only above it (lnerf_internal.h
+    // kXrowLast); every other row may fall kXrowD0 binades short of E_l before it is one
+    const bool tail = st && valid && !a.head_fit && (ls % a.S) == a.S - 1;
+    const int dmax = tail ? kXrowLast : kXrowD0;
     // PL = 2: layer l's weight exponent shift in lane l (read with readlane per pass); a pass's
     // accumulators carry 2^(ex + ew), removed exactly (powers of two) in its epilogue
     const int wexp_lane = (PL == 2 && lane < a.L) ? wshift_of(a.wexp[lane]) : 0;
@@ -968,6 +978,7 @@ k16_fwd_bwd_kernel(K16Args a) {
                     act[o][i] = relu_bit(v, o >= 8 ? mhi : mlo);
                 }
             }
+
             const unsigned long long mb = ((unsigned long long)mhi << 32) | mlo;
             if (st) mask_w[(size_t)l * NW * 64] = mb;
             PROF_ADD(kPfFwdEpi, t_fe);
@@ -1015,7 +1026,7 @@ k16_fwd_bwd_kernel(K16Args a) {
         PROF_T(t_b);
         const unsigned long long mb = mask_w[(size_t)(l - 1) * NW * 64];   // in flight over the pass
         const float xm = sample_max<false>(act);
-        store_emin(a, l, exa.get(l), store_sexp(a, l, 1, xm));
+        store_emin(a, l, exa.get(l), store_sexp(a, l, 1, xm, dmax), tail);
         int ex = shift_of(xm);
         if (PL == 2 && l == a.L - 1) {
             // the head: G's slab as it is (one k-step), then the pass on the column-scaled G row
@@ -1047,7 +1058,7 @@ k16_fwd_bwd_kernel(K16Args a) {
         // d_layer_input = G_0 W_0^T (ENCODED mode); the pass also writes G_0's slab
         zero_tiles(out);
         const float xm = sample_max<false>(act);
-        store_emin(a, 0, exa.get(0), store_sexp(a, 0, 1, xm));
+        store_emin(a, 0, exa.get(0), store_sexp(a, 0, 1, xm, dmax), tail);
         int ex = shift_of(xm);
         float* g0s = g0;
         if (PL == 2 && a.L == 1) {
@@ -1071,7 +1082,7 @@ k16_fwd_bwd_kernel(K16Args a) {
                 }
         }
     } else {
-        store_emin(a, 0, exa.get(0), store_sexp(a, 0, 1, sample_max<false>(act)));
+        store_emin(a, 0, exa.get(0), store_sexp(a, 0, 1, sample_max<false>(act), dmax), tail);
 #pragma unroll
         for (int s = 0; s < 8; ++s)
             if (s < a.ks_b[0]) store_slab_step(g0 + s * 1024, act[2 * s], act[2 * s + 1]);
@@ -1320,7 +1331,7 @@ void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lner
     a.planes = p.x6;
     a.wexp = p.wexp16;
     a.hexp = p.hexp16;
-    a.sexp = p.sexp;
+    a.sexp = (unsigned char*)p.sexp;
     a.rpad = p.num_wg * p.tile;
     a.epart = p.epart;
     // the chunk stream: forward 0..L-1, backward L-1..1 (training), backward 0 (d_x); chunks of

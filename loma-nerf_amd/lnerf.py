@@ -46,7 +46,7 @@ EXPORTED_SYMBOLS = [
     "mult_a_b", "lnerf_last_error", "lnerf_version", "lnerf_ctx_create", "lnerf_ctx_destroy",
     "lnerf_workspace_bytes", "lnerf_train_step", "lnerf_render", "lnerf_scale_by_device_scalar",
     "lnerf_adam_update", "lnerf_ctx_timings", "lnerf_get_rays", "lnerf_ctx_last_path",
-    "lnerf_ctx_set_option", "lnerf_ctx_relu_masks", "lnerf_build_knobs",
+    "lnerf_ctx_set_option", "lnerf_ctx_relu_masks", "lnerf_build_knobs", "lnerf_ctx_exceptional_rows",
 ]
 
 # lnerf_ctx_last_path bits
@@ -165,12 +165,17 @@ def configure(lib: ctypes.CDLL) -> None:
     lib.lnerf_ctx_last_path.argtypes = [ctypes.c_void_p]
     lib.lnerf_ctx_set_option.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
     lib.lnerf_ctx_relu_masks.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    if hasattr(lib, "lnerf_ctx_exceptional_rows"):   # (older in-tree A/B builds lack it)
+        lib.lnerf_ctx_exceptional_rows.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong),
+                                                   ctypes.POINTER(ctypes.c_longlong)]
     lib.lnerf_get_rays.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(ctypes.c_double), ctypes.c_void_p, ctypes.c_void_p]
     for name in ("lnerf_ctx_timings", "lnerf_ctx_last_path", "lnerf_ctx_set_option", "lnerf_ctx_relu_masks",
+                 "lnerf_ctx_exceptional_rows",
                  "lnerf_ctx_create", "lnerf_train_step", "lnerf_render",
                  "lnerf_scale_by_device_scalar", "lnerf_adam_update", "lnerf_get_rays"):
-        getattr(lib, name).restype = ctypes.c_int
+        if hasattr(lib, name):
+            getattr(lib, name).restype = ctypes.c_int
 
 
 def build_knobs() -> int:
@@ -341,6 +346,14 @@ class Engine:
             raise RuntimeError(f"lnerf_ctx_timings: {last_error()}")
         keys = ("pack", "fused", "loss", "dw", "reduce", "total")
         return {keys[i]: out[i] for i in range(n)}
+
+    def exceptional_rows(self, split=False):
+        """Rows (summed over layers) the last fp16x3 training step multiplied on the bf16x6 split
+        (lnerf_ctx_exceptional_rows; synchronises); split=True: (rows, of them rays' last samples)."""
+        n, t = ctypes.c_longlong(0), ctypes.c_longlong(0)
+        if self.lib.lnerf_ctx_exceptional_rows(self.ctx, ctypes.byref(n), ctypes.byref(t)) != 0:
+            raise RuntimeError(f"lnerf_ctx_exceptional_rows: {last_error()}")
+        return (int(n.value), int(t.value)) if split else int(n.value)
 
     def last_path(self) -> dict:
         """The kernels the last train_step/render ran (lnerf_ctx_last_path)."""

@@ -50,7 +50,25 @@ typedef _Float16 hf4 __attribute__((ext_vector_type(4)));
 #define LNERF_DW16_XROW 1
 #endif
 
-constexpr int kThreads = 512;
+// WAVES: waves per dW workgroup. 8 (round 5): two per SIMD, 256 registers each -- a 2 x 4 tile block
+// per wave, three half-blocks of loads in flight that the compiler partly spills to scratch (and
+// then waits for with vmcnt(0)); 4 (round 6 A/B): one wave per SIMD with the whole 512-entry
+// register file -- a 4 x 4 tile block per wave and the same loads in registers (no spills), twice the
+// rounds per thread. Measured in-process on the bench batch: k2 0.866-0.899 ms against 0.765 for 8
+// waves (k1 unchanged): without a partner wave the split VALU, the image writes and the
+// per-half-block barrier no longer issue under another wave's MFMAs; the spills were not the bound.
+#ifndef LNERF_DW16_WAVES
+#define LNERF_DW16_WAVES 8
+#endif
+constexpr int kWavesDw = LNERF_DW16_WAVES;
+static_assert(kWavesDw == 16 || kWavesDw == 8 || kWavesDw == 4, "dW workgroups of 16, 8 or 4 waves");
+constexpr int kThreads = 64 * kWavesDw;
+// a 32-feature tile's half-block is 128 threads' loads (4 features of one sample each); the
+// workgroup's kTileGroups thread groups take kRPO tiles of an operand each: rounds 0 .. kRPO - 1
+// load A tiles, kRPO .. 2 kRPO - 1 G tiles, round i tile kTileGroups (i % kRPO) + t / 128
+constexpr int kTileGroups = kWavesDw / 2;
+constexpr int kRPO = 8 / kTileGroups;
+constexpr int kRounds = 2 * kRPO;
 constexpr int kRows = 512;                  // A rows [0, 256) and G rows [256, 512) of the image
 // one plane of a half-block: [16 samples][512 features] 16-bit, each sample's row padded by 64 B
 // so that the 4 sample rows one ds_read_b64_tr_b16 lane group reads start 16 banks apart
@@ -98,8 +116,9 @@ struct Dw16Args {
 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
-// The 16 B that thread t loads in round i (0..3) of a half-block: rounds 0, 1 are A tiles 0-3 and
-// 4-7, rounds 2, 3 G tiles 0-3 and 4-7; tile 4 (i & 1) + t / 128, and inside the tile's 512-float
+// The 16 B that thread t loads in round i of a half-block (8 waves: rounds 0, 1 are A tiles 0-3 and
+// 4-7, rounds 2, 3 G tiles 0-3 and 4-7; tile 4 (i & 1) + t / 128 -- generally kTileGroups (i % kRPO)
+// + t / 128, A for i < kRPO), and inside the tile's 512-float
 // half-block [h][n][16 f] (k16's sample-major layout) the floats 4 (t % 128) ..+3 = features
 // 16 h + 4 (t % 4) ..+3 of sample n, with h = (t / 64) % 2 and n = (t % 64) / 4. A slab block is
 // [tile][half-block 2][512]. The per-thread part of the offset is fixed (RowMap), the half-block
@@ -109,8 +128,8 @@ struct RowMap {
     int hstride;     // floats between the two half-blocks of a 32-sample block's tile
     int rowo;        // the thread's first feature inside its 32-feature tile (4 consecutive)
     int isamp;       // the thread's sample inside the half-block (its LDS image row)
-    int tile[4];     // wave-uniform: the 32-feature tile of round i (tile 0 for tiles past the layer)
-    bool ok[4];      // wave-uniform: the tile exists in this layer (else it is never split)
+    int tile[kRounds];   // wave-uniform: the 32-feature tile of round i (tile 0 for tiles past the layer)
+    bool ok[kRounds];    // wave-uniform: the tile exists in this layer (else it is never split)
 };
 
 __device__ __forceinline__ RowMap row_map(int kt, int nt) {
@@ -122,9 +141,9 @@ __device__ __forceinline__ RowMap row_map(int kt, int nt) {
     m.isamp = (t & 63) >> 2;
     const int w2 = wave_id() >> 1;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int tl = 4 * (i & 1) + w2;
-        m.ok[i] = tl < (i < 2 ? kt : nt);
+    for (int i = 0; i < kRounds; ++i) {
+        const int tl = kTileGroups * (i % kRPO) + w2;
+        m.ok[i] = tl < (i < kRPO ? kt : nt);
         m.tile[i] = m.ok[i] ? tl : 0;
     }
     return m;
@@ -132,11 +151,11 @@ __device__ __forceinline__ RowMap row_map(int kt, int nt) {
 
 // image feature row of round i's 4 values for thread t (A rows 0..255, G rows 256..511)
 __device__ __forceinline__ int image_row(int i, const RowMap& m) {
-    return (i < 2 ? 0 : 256) + 32 * (4 * (i & 1) + (threadIdx.x >> 7)) + m.rowo;
+    return (i < kRPO ? 0 : 256) + 32 * (kTileGroups * (i % kRPO) + (threadIdx.x >> 7)) + m.rowo;
 }
 
 struct Loads {
-    fx4 v[4];
+    fx4 v[kRounds];
     unsigned e;   // the sample's k1 word (sexp_xa, sexp_xg, sexp_dmax)
 };
 
@@ -185,7 +204,7 @@ __device__ __forceinline__ void issue_loads(const float* A, const float* G, cons
         // of a 3-element vector type keeps only its first element)
         const unsigned char* pa = (const unsigned char*)A + ((size_t)blk * kt * 3072 + half * 1536 + 12 * (threadIdx.x & 127));
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < kRPO; ++i) {
             const unsigned* q = (const unsigned*)(pa + m.tile[i] * 3072);
             L.v[i] = fx4{__builtin_bit_cast(float, __builtin_nontemporal_load(q)),
                          __builtin_bit_cast(float, __builtin_nontemporal_load(q + 1)),
@@ -194,10 +213,10 @@ __device__ __forceinline__ void issue_loads(const float* A, const float* G, cons
     } else {
         const float* pa = A + (size_t)blk * kt * 1024 + half * m.hstride;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) L.v[i] = __builtin_nontemporal_load((const fx4*)(pa + m.tile[i] * 1024 + m.lane));
+        for (int i = 0; i < kRPO; ++i) L.v[i] = __builtin_nontemporal_load((const fx4*)(pa + m.tile[i] * 1024 + m.lane));
     }
 #pragma unroll
-    for (int i = 2; i < 4; ++i) L.v[i] = __builtin_nontemporal_load((const fx4*)(pg + m.tile[i] * 1024 + m.lane));
+    for (int i = kRPO; i < kRounds; ++i) L.v[i] = __builtin_nontemporal_load((const fx4*)(pg + m.tile[i] * 1024 + m.lane));
 }
 
 // The 4 values of an int24 A round (k1 store_slab_step24): 3 dwords holding the low 24 bits of
@@ -239,7 +258,7 @@ template <int PL>
 __device__ __forceinline__ void write_planes_row(const fx4& v, int i, unsigned char* img, float sa, float sg,
                                                  const RowMap& m) {
     unsigned char* p = img + m.isamp * kImgRow + 8 * ((image_row(i, m) >> 2) ^ swz(m.isamp));
-    const float sc = i < 2 ? sa : sg;
+    const float sc = i < kRPO ? sa : sg;
     if constexpr (PL == 2) {
         typedef unsigned u2 __attribute__((ext_vector_type(2)));
         unsigned h0, l0, h1, l1;
@@ -296,7 +315,7 @@ __device__ __forceinline__ void sample_scales(unsigned e, int E, float& sa, floa
 template <int PL>
 __device__ __forceinline__ fx4 round_values(const Loads& L, int i) {
     if constexpr (a24k(PL)) {
-        if (i >= 2) return L.v[i];
+        if (i >= kRPO) return L.v[i];
         fx4 v = decode_a24(L.v[i]);
         const bool marked = sexp_xa(L.e) == kSexpNonFinite;
         if (__builtin_expect(__builtin_amdgcn_ballot_w64(marked) != 0, 0)) {
@@ -318,7 +337,7 @@ __device__ __forceinline__ void write_planes(const Loads& L, unsigned char* img,
     float sa, sg;
     sample_scales<PL>(L.e, E, sa, sg);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) write_planes_row<PL>(round_values<PL>(L, i), i, img, sa, sg, m);
+    for (int i = 0; i < kRounds; ++i) write_planes_row<PL>(round_values<PL>(L, i), i, img, sa, sg, m);
 }
 
 __device__ __forceinline__ fx16 mfma32(const bf8& a, const bf8& b, fx16 c) {
@@ -374,6 +393,41 @@ __device__ __forceinline__ fx16 mma_tile(const bf8 (&ap)[nplanes(PL)], const bf8
     return c;
 }
 
+// One output column tile j's products for all TI row tiles, product-major: the TI accumulators
+// take their k-th product in turn, so consecutive MFMAs never wait on each other's result (a
+// dependent 32x32x16 MFMA pair stalls for the first one's passes; two waves per SIMD hide that with
+// the partner's MFMAs, one wave per SIMD has only its own other tiles). Round-6 default for every
+// wave count: the same sums per accumulator bit for bit; 8 waves measured k2 0.761 ms against
+// 0.765 tile-major (in-process A/B).
+#ifndef LNERF_DW16_PMAJOR
+#define LNERF_DW16_PMAJOR 1
+#endif
+template <int PL, int TI, int TJ>
+__device__ __forceinline__ void mma_col(const bf8 (&ap)[TI][nplanes(PL)], const bf8 (&gp)[nplanes(PL)],
+                                        fx16 (&acc)[TI][TJ], int j) {
+    if constexpr (!LNERF_DW16_PMAJOR) {
+#pragma unroll
+        for (int i = 0; i < TI; ++i) acc[i][j] = mma_tile<PL>(ap[i], gp, acc[i][j]);
+    } else if constexpr (PL == 2) {
+        // (a_hi g_lo, a_lo g_hi, a_hi g_hi): small terms first, as mma_tile
+#pragma unroll
+        for (int i = 0; i < TI; ++i) acc[i][j] = mfma32h(ap[i][0], gp[1], acc[i][j]);
+#pragma unroll
+        for (int i = 0; i < TI; ++i) acc[i][j] = mfma32h(ap[i][1], gp[0], acc[i][j]);
+#pragma unroll
+        for (int i = 0; i < TI; ++i) acc[i][j] = mfma32h(ap[i][0], gp[0], acc[i][j]);
+    } else if constexpr (PL == 1) {
+#pragma unroll
+        for (int i = 0; i < TI; ++i) acc[i][j] = mfma32(ap[i][0], gp[0], acc[i][j]);
+    } else {
+        constexpr int pa[6] = {0, 1, 2, 1, 0, 0}, pg[6] = {2, 1, 0, 0, 1, 0};
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+#pragma unroll
+            for (int i = 0; i < TI; ++i) acc[i][j] = mfma32(ap[i][pa[k]], gp[pg[k]], acc[i][j]);
+    }
+}
+
 // The wave's TI x TJ tile block (TI 32-row tiles of A, TJ of G) on one half-block image, with
 // the split of the next half-block interleaved (round k beside output column tile k), so the
 // VALU split issues under the MFMAs. Branch-free (ACTIVE is a template parameter; past the
@@ -395,22 +449,32 @@ __device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int 
 #pragma unroll
             for (int p = 0; p < NP; ++p) ap[i][p] = read_frag((unsigned char*)fl + p * kPlaneBytes + frag_off(a0 + 32 * i));
     }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    // RPS split rounds beside each output column tile (8 waves: one; 4 waves: kRounds / TJ)
+    constexpr int RPS = (kWavesDw == 8 || TJ >= kRounds) ? 1 : (kRounds + TJ - 1) / TJ;
+    constexpr int NR = (kRounds + RPS - 1) / RPS;
+    constexpr int NK = NR > TJ ? NR : TJ;
+    auto split = [&](int k) {
         // rows past the layer's tiles are never read: skip their split (wave-uniform: a wave's
         // values of a round lie in one 32-feature tile); FULL layers need no branch
-        if (!LNERF_DW16_SPLIT_LATE && (FULL || m.ok[k])) write_planes_row<PL>(round_values<PL>(nl, k), k, nxt, sa, sg, m);
+#pragma unroll
+        for (int r = 0; r < RPS; ++r) {
+            const int i = k * RPS + r;
+            if (i < kRounds && (FULL || m.ok[i])) write_planes_row<PL>(round_values<PL>(nl, i), i, nxt, sa, sg, m);
+        }
+    };
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+        if (!LNERF_DW16_SPLIT_LATE) split(k);
         if constexpr (ACTIVE) {
             if (k < TJ) {
                 const int j = k < TJ ? k : 0;
                 bf8 gp[NP];
 #pragma unroll
                 for (int p = 0; p < NP; ++p) gp[p] = read_frag((unsigned char*)fl + p * kPlaneBytes + frag_off(256 + g0 + 32 * j));
-#pragma unroll
-                for (int i = 0; i < TI; ++i) acc[i][j] = mma_tile<PL>(ap[i], gp, acc[i][j]);
+                mma_col<PL, TI, TJ>(ap, gp, acc, j);
             }
         }
-        if (LNERF_DW16_SPLIT_LATE && (FULL || m.ok[k])) write_planes_row<PL>(round_values<PL>(nl, k), k, nxt, sa, sg, m);
+        if (LNERF_DW16_SPLIT_LATE) split(k);
     }
 }
 
@@ -421,15 +485,15 @@ __device__ __forceinline__ void block_mma(const unsigned char* img, int a0, int 
 template <int PL, int TI, int TJ, bool ACTIVE, bool FULL, int I>
 __device__ __forceinline__ void hb_step3(const float* A, const float* G, const unsigned* se, int kt, int nt,
                                          const RowMap& m, int hb, int hb0, int hb1, int a0, int g0,
-                                         fx16 (&acc)[TI][TJ], Loads& L0, Loads& L1, Loads& L2, fx4 (&dbs)[2],
+                                         fx16 (&acc)[TI][TJ], Loads& L0, Loads& L1, Loads& L2, fx4 (&dbs)[kRPO],
                                          unsigned char* lds, int E, bool& xany) {
     constexpr int kIB = image_bytes<PL>();
     Loads& fr = I == 0 ? L0 : I == 1 ? L1 : L2;
     const Loads& nx = I == 0 ? L1 : I == 1 ? L2 : L0;
     issue_loads<a24k(PL)>(A, G, se, kt, nt, m, hb + 3, hb1, fr);
     if (hb + 1 < hb1) {
-        dbs[0] += nx.v[2];
-        dbs[1] += nx.v[3];
+#pragma unroll
+        for (int i = 0; i < kRPO; ++i) dbs[i] += nx.v[kRPO + i];
     }
     const int cur = (hb - hb0) & 1;
     block_mma<PL, TI, TJ, ACTIVE, FULL>(lds + cur * kIB, a0, g0, acc, nx, lds + (cur ^ 1) * kIB, m, E, hb + 1 < hb1);
@@ -441,7 +505,7 @@ __device__ __forceinline__ void hb_step3(const float* A, const float* G, const u
 template <int PL, int TI, int TJ, bool ACTIVE, bool FULL>
 __device__ __forceinline__ void hb_loop3(const float* A, const float* G, const unsigned* se, int kt, int nt,
                                          const RowMap& m, int hb0, int hb1, int a0, int g0, fx16 (&acc)[TI][TJ],
-                                         Loads& L0, Loads& L1, Loads& L2, fx4 (&dbs)[2], unsigned char* lds,
+                                         Loads& L0, Loads& L1, Loads& L2, fx4 (&dbs)[kRPO], unsigned char* lds,
                                          int E, bool& xany) {
     // whole triples only (one loop body; remainder copies make the compiler spill the
     // accumulators): the steps past hb1 split zero-scaled (zero) planes and add nothing
@@ -458,15 +522,15 @@ __device__ __forceinline__ void hb_loop3(const float* A, const float* G, const u
 template <int PL, int TI, int TJ, bool ACTIVE, bool FULL, int I>
 __device__ __forceinline__ void hb_step2(const float* A, const float* G, const unsigned* se, int kt, int nt,
                                          const RowMap& m, int hb, int hb0, int hb1, int a0, int g0,
-                                         fx16 (&acc)[TI][TJ], Loads& L0, Loads& L1, fx4 (&dbs)[2],
+                                         fx16 (&acc)[TI][TJ], Loads& L0, Loads& L1, fx4 (&dbs)[kRPO],
                                          unsigned char* lds, int E, bool& xany) {
     constexpr int kIB = image_bytes<PL>();
     Loads& fr = I == 0 ? L0 : L1;
     const Loads& nx = I == 0 ? L1 : L0;
     issue_loads<a24k(PL)>(A, G, se, kt, nt, m, hb + 2, hb1, fr);
     if (hb + 1 < hb1) {
-        dbs[0] += nx.v[2];
-        dbs[1] += nx.v[3];
+#pragma unroll
+        for (int i = 0; i < kRPO; ++i) dbs[i] += nx.v[kRPO + i];
     }
     const int cur = (hb - hb0) & 1;
     block_mma<PL, TI, TJ, ACTIVE, FULL>(lds + cur * kIB, a0, g0, acc, nx, lds + (cur ^ 1) * kIB, m, E, hb + 1 < hb1);
@@ -478,7 +542,7 @@ __device__ __forceinline__ void hb_step2(const float* A, const float* G, const u
 template <int PL, int TI, int TJ, bool ACTIVE, bool FULL>
 __device__ __forceinline__ void hb_loop2(const float* A, const float* G, const unsigned* se, int kt, int nt,
                                          const RowMap& m, int hb0, int hb1, int a0, int g0, fx16 (&acc)[TI][TJ],
-                                         Loads& L0, Loads& L1, fx4 (&dbs)[2], unsigned char* lds, int E,
+                                         Loads& L0, Loads& L1, fx4 (&dbs)[kRPO], unsigned char* lds, int E,
                                          bool& xany) {
     for (int hb = hb0; hb < hb1; hb += 2) {
         hb_step2<PL, TI, TJ, ACTIVE, FULL, 0>(A, G, se, kt, nt, m, hb, hb0, hb1, a0, g0, acc, L0, L1, dbs, lds, E, xany);
@@ -501,7 +565,7 @@ __device__ __forceinline__ void gather_loads(const float* A, const float* G, con
     if constexpr (A24) {
         const unsigned char* pa = (const unsigned char*)A + ((size_t)blk * kt * 3072 + half * 1536 + 12 * u);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < kRPO; ++i) {
             const unsigned* q = (const unsigned*)(pa + m.tile[i] * 3072);
             L.v[i] = fx4{__builtin_bit_cast(float, q[0]), __builtin_bit_cast(float, q[1]),
                          __builtin_bit_cast(float, q[2]), 0.0f};
@@ -509,10 +573,10 @@ __device__ __forceinline__ void gather_loads(const float* A, const float* G, con
     } else {
         const float* pa = A + (size_t)blk * kt * 1024 + half * 512 + 4 * u;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) L.v[i] = *(const fx4*)(pa + m.tile[i] * 1024);
+        for (int i = 0; i < kRPO; ++i) L.v[i] = *(const fx4*)(pa + m.tile[i] * 1024);
     }
 #pragma unroll
-    for (int i = 2; i < 4; ++i) L.v[i] = *(const fx4*)(pg + m.tile[i] * 1024);
+    for (int i = kRPO; i < kRounds; ++i) L.v[i] = *(const fx4*)(pg + m.tile[i] * 1024);
 }
 
 // the wave's TI x TJ tile block of one image (no split interleaved)
@@ -529,8 +593,7 @@ __device__ __forceinline__ void mma_block(const unsigned char* img, int a0, int 
         bf8 gp[NP];
 #pragma unroll
         for (int p = 0; p < NP; ++p) gp[p] = read_frag((unsigned char*)img + p * kPlaneBytes + frag_off(256 + g0 + 32 * j));
-#pragma unroll
-        for (int i = 0; i < TI; ++i) acc[i][j] = mma_tile<PL>(ap[i], gp, acc[i][j]);
+        mma_col<PL, TI, TJ>(ap, gp, acc, j);
     }
 }
 
@@ -542,23 +605,24 @@ __device__ __forceinline__ void mma_block(const unsigned char* img, int a0, int 
 // previous group is split. `any`: some thread's main loop met an exceptional row; a split that met
 // none (the bench batch: all but a handful) skips the scan after two barriers. Deterministic: the
 // groups follow position order. Returns the rows multiplied and, of them, rays' last samples.
-constexpr int kXrowRing = 4096;   // > 15 pending + 4 x 512 listed per scan step
+constexpr int kXrowRing = 8 * kThreads;   // > 15 pending + 4 x kThreads listed per scan step
 template <int TI, int TJ>
 __device__ __forceinline__ int2 xrow_pass(const float* A, const float* G, const unsigned* se, int KT, int NT,
                                           const RowMap& m, int hb0, int hb1, int a0, int g0, bool active,
                                           fx16 (&acc)[TI][TJ], unsigned char* lds, int E, bool any) {
     constexpr int PX = kXrowPL;
     int* ring = (int*)(lds + image_bytes<PX>());
-    int* wcnt = ring + kXrowRing;   // [2: rows, last samples][4 scan rounds][8 waves], then the any flags
+    int* wcnt = ring + kXrowRing;   // [2: rows, last samples][4 scan rounds][waves], then the any flags
+    constexpr int W = kWavesDw;
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
     const int p0 = hb0 * 16, p1 = hb1 * 16;
     const bool wany = __builtin_amdgcn_ballot_w64(any) != 0;
     __syncthreads();   // every wave is done with the fp16x3 images
-    if (lane == 0) wcnt[64 + wave] = wany ? 1 : 0;
+    if (lane == 0) wcnt[8 * W + wave] = wany ? 1 : 0;
     __syncthreads();
     int anyw = 0;
 #pragma unroll
-    for (int w = 0; w < 8; ++w) anyw |= wcnt[64 + w];
+    for (int w = 0; w < kWavesDw; ++w) anyw |= wcnt[8 * W + w];
     if (!anyw) return int2{0, 0};
     int head = 0, tail = 0, ntail = 0;   // workgroup-uniform (ring slot = index % kXrowRing)
     for (int base = p0; base < p1; base += 4 * kThreads) {
@@ -577,8 +641,8 @@ __device__ __forceinline__ int2 xrow_pass(const float* A, const float* G, const 
             bal[k] = __builtin_amdgcn_ballot_w64(f[k]);
             const unsigned long long bt = __builtin_amdgcn_ballot_w64(tl[k]);
             if (lane == 0) {
-                wcnt[k * 8 + wave] = __builtin_popcountll(bal[k]);
-                wcnt[32 + k * 8 + wave] = __builtin_popcountll(bt);
+                wcnt[k * W + wave] = __builtin_popcountll(bal[k]);
+                wcnt[4 * W + k * W + wave] = __builtin_popcountll(bt);
             }
         }
         __syncthreads();
@@ -586,11 +650,11 @@ __device__ __forceinline__ int2 xrow_pass(const float* A, const float* G, const 
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             int mine = off;
-            for (int w = 0; w < 8; ++w) {
-                const int c = wcnt[k * 8 + w];
+            for (int w = 0; w < kWavesDw; ++w) {
+                const int c = wcnt[k * W + w];
                 mine += w < wave ? c : 0;
                 off += c;
-                ntail += wcnt[32 + k * 8 + w];
+                ntail += wcnt[4 * W + k * W + w];
             }
             if (f[k]) {
                 const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(bal[k] >> 32),
@@ -620,7 +684,7 @@ __device__ __forceinline__ int2 xrow_pass(const float* A, const float* G, const 
                 sa = pc < 0 ? 0.0f : sa;
                 sg = pc < 0 ? 0.0f : sg;
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < kRounds; ++i)
                     if (m.ok[i]) write_planes_row<PX>(round_values<PX>(Lc, i), i, lds, sa, sg, m);
                 __syncthreads();
                 if (active) mma_block<PX, TI, TJ>(lds, a0, g0, acc);
@@ -654,7 +718,9 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
 #pragma unroll
         for (int j = 0; j < TJ; ++j) acc[i][j] = fx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     // db: this thread's G values are features image_row(i) - 256 ..+3 of one sample, i = 2, 3
-    fx4 dbs[2] = {fx4{0.0f, 0.0f, 0.0f, 0.0f}, fx4{0.0f, 0.0f, 0.0f, 0.0f}};
+    fx4 dbs[kRPO];
+#pragma unroll
+    for (int i = 0; i < kRPO; ++i) dbs[i] = fx4{0.0f, 0.0f, 0.0f, 0.0f};
 
     const float* A = a.act + a.a_off[l];
     const float* G = a.grad + a.g_off[l];
@@ -670,8 +736,8 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
     issue_loads<a24k(PL)>(A, G, se, KT, NT, m, hb0, hb1, L0);
     issue_loads<a24k(PL)>(A, G, se, KT, NT, m, hb0 + 1, hb1, L1);
     if (hb0 < hb1) {
-        dbs[0] += L0.v[2];
-        dbs[1] += L0.v[3];
+#pragma unroll
+        for (int i = 0; i < kRPO; ++i) dbs[i] += L0.v[kRPO + i];
         write_planes<PL>(L0, lds, E, m);
         if constexpr (PL == 2 && LNERF_DW16_XROW) xany = xrow(L0.e, E);
     }
@@ -687,8 +753,8 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
     issue_loads<a24k(PL)>(A, G, se, KT, NT, m, hb0 + 1, hb1, L1);
     issue_loads<a24k(PL)>(A, G, se, KT, NT, m, hb0 + 2, hb1, L2);
     if (hb0 < hb1) {
-        dbs[0] += L0.v[2];
-        dbs[1] += L0.v[3];
+#pragma unroll
+        for (int i = 0; i < kRPO; ++i) dbs[i] += L0.v[kRPO + i];
         write_planes<PL>(L0, lds, E, m);
         if constexpr (PL == 2 && LNERF_DW16_XROW) xany = xrow(L0.e, E);
     }
@@ -732,9 +798,9 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
     float* red = (float*)lds;
     __syncthreads();   // the image buffers are free: every wave is past its last MFMA reads
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < kRPO; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) red[(image_row(2 + i, m) - 256 + j) * 16 + m.isamp] = dbs[i][j];
+        for (int j = 0; j < 4; ++j) red[(image_row(kRPO + i, m) - 256 + j) * 16 + m.isamp] = dbs[i][j];
     __syncthreads();
     if (tid < NT * 32) {
         const float* q = red + tid * 16;
@@ -745,12 +811,27 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
     }
 }
 
-// Block shape per layer: the smallest of 1x1, 1x2, 2x4 tiles that needs at most 8 waves, so
-// small layers (the head, layer 0) spread over all SIMDs instead of a few waves.
+// Block shape per layer: the smallest tile block that needs at most kWavesDw waves, so small
+// layers (the head, layer 0) spread over all SIMDs instead of a few waves. 8 waves: 1x1, 1x2, 2x4;
+// 4 waves: 1x1, 2x1, 1x2, 2x2, 4x4 (the 8 x 8 hidden layers).
 __host__ __device__ __forceinline__ int dw_shape(int kt, int nt) {
-    if (kt * nt <= 8) return 0;
-    if (kt * ((nt + 1) / 2) <= 8) return 1;
-    return 2;
+    auto fits = [&](int ti, int tj) { return ((kt + ti - 1) / ti) * ((nt + tj - 1) / tj) <= kWavesDw; };
+    if (kWavesDw == 8) {
+        if (fits(1, 1)) return 0;
+        if (fits(1, 2)) return 1;
+        return 2;
+    }
+    if (kWavesDw == 16) {
+        if (fits(1, 1)) return 0;
+        if (fits(1, 2)) return 1;
+        if (fits(2, 1)) return 3;
+        return 4;
+    }
+    if (fits(1, 1)) return 0;
+    if (fits(2, 1)) return 3;
+    if (fits(1, 2)) return 1;
+    if (fits(2, 2)) return 4;
+    return 5;
 }
 
 // LDS of a dW workgroup: the two half-block images; under fp16x3 the exceptional rows' bf16x6 image
@@ -758,20 +839,38 @@ __host__ __device__ __forceinline__ int dw_shape(int kt, int nt) {
 template <int PL>
 constexpr int dw_lds_bytes() {
     constexpr int main = 2 * image_bytes<PL>();
-    constexpr int xr = PL == 2 && LNERF_DW16_XROW ? image_bytes<kXrowPL>() + (kXrowRing + 72) * 4 : 0;
+    constexpr int xr = PL == 2 && LNERF_DW16_XROW ? image_bytes<kXrowPL>() + (kXrowRing + 9 * kWavesDw) * 4 : 0;
     return main > xr ? main : xr;
 }
 
 template <int PL>
-__global__ void __launch_bounds__(kThreads, 1) dw16_kernel(Dw16Args a) {
+__global__ void __launch_bounds__(kThreads, 1) __attribute__((amdgpu_waves_per_eu(kWavesDw / 4, kWavesDw / 4)))
+dw16_kernel(Dw16Args a) {
     __shared__ __attribute__((aligned(16))) unsigned char lds[dw_lds_bytes<PL>()];
     int li = 0;
     while (li + 1 < a.nl && (int)blockIdx.x >= a.wg_off[li + 1]) ++li;
     const int l = a.lid[li], sp = blockIdx.x - a.wg_off[li];
-    switch (dw_shape(a.kt[l], a.nt[l])) {
-        case 0: dw_split<PL, 1, 1>(a, l, sp, lds); break;
-        case 1: dw_split<PL, 1, 2>(a, l, sp, lds); break;
-        default: dw_split<PL, 2, 4>(a, l, sp, lds); break;
+    if constexpr (kWavesDw == 8) {
+        switch (dw_shape(a.kt[l], a.nt[l])) {
+            case 0: dw_split<PL, 1, 1>(a, l, sp, lds); break;
+            case 1: dw_split<PL, 1, 2>(a, l, sp, lds); break;
+            default: dw_split<PL, 2, 4>(a, l, sp, lds); break;
+        }
+    } else if constexpr (kWavesDw == 16) {
+        switch (dw_shape(a.kt[l], a.nt[l])) {
+            case 0: dw_split<PL, 1, 1>(a, l, sp, lds); break;
+            case 1: dw_split<PL, 1, 2>(a, l, sp, lds); break;
+            case 3: dw_split<PL, 2, 1>(a, l, sp, lds); break;
+            default: dw_split<PL, 2, 2>(a, l, sp, lds); break;
+        }
+    } else {
+        switch (dw_shape(a.kt[l], a.nt[l])) {
+            case 0: dw_split<PL, 1, 1>(a, l, sp, lds); break;
+            case 3: dw_split<PL, 2, 1>(a, l, sp, lds); break;
+            case 1: dw_split<PL, 1, 2>(a, l, sp, lds); break;
+            case 4: dw_split<PL, 2, 2>(a, l, sp, lds); break;
+            default: dw_split<PL, 4, 4>(a, l, sp, lds); break;
+        }
     }
 }
 
@@ -823,7 +922,8 @@ __global__ void __launch_bounds__(1024) k1_reduce_kernel(const int* __restrict__
 unsigned dw16_build_knobs() {
     return (LNERF_DW16_SPLIT_LATE != 1 ? kKnobDwSplitLate : 0u) | (LNERF_DW16_DEPTH != 3 ? kKnobDwDepth : 0u) |
            (LNERF_DW16_SWZ != 1 ? kKnobDwSwz : 0u) | (LNERF_A24 != 1 ? kKnobA24 : 0u) |
-           (LNERF_DW16_XROW != 1 ? kKnobDwXrow : 0u);
+           (LNERF_DW16_XROW != 1 ? kKnobDwXrow : 0u) |
+           (LNERF_DW16_WAVES != 8 || !LNERF_DW16_PMAJOR ? kKnobDwWaves : 0u);
 }
 
 void dw16_launch(const FusedPlan& p, hipStream_t s) {

@@ -100,7 +100,7 @@ enum : unsigned {
     kKnobK16Prio = 1u << 4, kKnobK16Spread = 1u << 5, kKnobProf = 1u << 6, kKnobA24 = 1u << 7,
     kKnobK16Only = 1u << 8, kKnobDwSplitLate = 1u << 9, kKnobDwDepth = 1u << 10, kKnobDwSwz = 1u << 11,
     kKnobK16Pin = 1u << 12, kKnobK16FdSrc = 1u << 13, kKnobKrStagger = 1u << 15, kKnobDwXrow = 1u << 17,
-    kKnobKrSched = 1u << 18, kKnobKrDist = 1u << 19, kKnobPeDoubling = 1u << 20, kKnobK16OneChunk = 1u << 22, kKnobK16WaveComp = 1u << 23, kKnobK16EpiFma = 1u << 24,
+    kKnobKrSched = 1u << 18, kKnobDwWaves = 1u << 14, kKnobKrDist = 1u << 19, kKnobPeDoubling = 1u << 20, kKnobK16OneChunk = 1u << 22, kKnobK16WaveComp = 1u << 23, kKnobK16EpiFma = 1u << 24,
 };
 unsigned k16_build_knobs();
 unsigned dw16_build_knobs();

@@ -640,8 +640,11 @@ def main():
     if not args.generic and last_path and last_path.get("planes") == 2:
         n_x, n_last = t.eng.exceptional_rows(split=True)
         xrows = {"rows": n_x, "of_them_last_samples": n_last, "of": len(shapes) * N * S,
+                 "floor_guard_fired": t.eng.guard_fired(),
                  "note": "rows (summed over layers) that dw16 multiplied on the bf16x6 split instead of "
-                         "the fp16x3 one (lnerf_internal.h kXrowD0); measured on the last step"}
+                         "the fp16x3 one (lnerf_internal.h kXrowD0); floor_guard_fired: 1 if k1 met a hidden "
+                         "G element below fp16x3's floor and the step re-ran on bf16x6 (kGuardExp); both "
+                         "measured on the last step"}
     t.close()
 
     variants = variant_flags(args)

@@ -262,6 +262,14 @@ int lnerf_ctx_relu_masks(lnerf_ctx* ctx, unsigned char* out, size_t out_bytes, v
  * device. An extension (no loma counterpart). */
 int lnerf_ctx_exceptional_rows(lnerf_ctx* ctx, long long* rows, long long* last_samples);
 
+/* The fp16x3 floor guard of the last training step on `ctx`: *fired = 1 if k1 met a hidden-layer
+ * gradient element below what the fp16x3 split can carry (more than ~2^37 below its row's maximum,
+ * lnerf_internal.h kGuardExp) and the step was therefore re-run on the device on the bf16x6 split
+ * (every output of the step comes from that re-run), 0 if not, -1 if the step had no guard (an
+ * explicit precision flag, the generic path, LNERF_HEAD_FIT or LNERF_K16_W4). Synchronises the
+ * device. An extension (no loma counterpart). */
+int lnerf_ctx_guard_fired(lnerf_ctx* ctx, int* fired);
+
 /* Sets an engine option (LNERF_OPT_*) for later steps on `ctx`. Returns 0, or a negative code for
  * an unknown option or an out-of-range value. */
 int lnerf_ctx_set_option(lnerf_ctx* ctx, int option, int value);

@@ -706,9 +706,23 @@ extern "C" int lnerf_train_step(lnerf_ctx* ctx, const lnerf_mlp* mlp, const floa
         if (use_fused(*mlp, *batch, flags)) {
             const size_t bytes = fused_workspace_bytes(*mlp, batch->rays, batch->samples, true, ctx->dw_grid);
             FusedPlan p{};
-            fused_plan(p, *mlp, *batch, ctx->fused_ws.get(bytes), flags, true, ctx->dw_grid);
+            void* wsb = ctx->fused_ws.get(bytes);
+            fused_plan(p, *mlp, *batch, wsb, flags, true, ctx->dw_grid);
+            // the fp16x3 floor guard (lnerf_internal.h kGuardExp) under the default precision: the
+            // bf16x6 plan of the same step, run on the device only if k1 finds a hidden G element
+            // below fp16x3's floor (an explicit LNERF_MFMA_F16X3 asks for fp16x3 exactly; the mlp_fit
+            // head and the 64-sample workgroups have no bf16x6 k1)
+            const bool guarded = LNERF_GUARD && p.x6 == 2 && !(flags & (LNERF_MFMA_F16X3 | LNERF_K16_W4 | LNERF_HEAD_FIT));
+            FusedPlan px{};
+            if (guarded) {
+                fused_plan(px, *mlp, *batch, wsb, flags | LNERF_MFMA_BF16X6, true, ctx->dw_grid);
+                px.guard = nullptr;
+                px.gate = p.guard;
+            } else {
+                p.guard = nullptr;
+            }
             const bool timed = (flags & LNERF_TIMING) != 0;
-            fused_train_step(p, ws, bs, *batch, seed, flags, o, s, timed ? ctx->ev : nullptr);
+            fused_train_step(p, ws, bs, *batch, seed, flags, o, s, timed ? ctx->ev : nullptr, guarded ? &px : nullptr);
             check_launch("lnerf_train_step");
             ctx->timed = timed;
             ctx->last_path = path_bits(p, true);
@@ -820,6 +834,22 @@ extern "C" int lnerf_ctx_exceptional_rows(lnerf_ctx* ctx, long long* rows, long 
         }
         *rows = t;
         if (last_samples) *last_samples = l;
+    });
+}
+
+extern "C" int lnerf_ctx_guard_fired(lnerf_ctx* ctx, int* fired) {
+    return guard_int([&]() {
+        if (!ctx || !fired) fail("null argument");
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        if (!ctx->last_k16_train) fail("no k16 training step has run on this context since the last other call");
+        const FusedPlan& p = ctx->last_plan;
+        *fired = -1;   // no guard on that step (not the default fp16x3 precision)
+        if (!p.guard) return;
+        HIP_OK(hipSetDevice(ctx->device));
+        HIP_OK(hipDeviceSynchronize());
+        int w = 0;
+        HIP_OK(hipMemcpy(&w, p.guard, sizeof(int), hipMemcpyDeviceToHost));
+        *fired = w != 0 ? 1 : 0;
     });
 }
 

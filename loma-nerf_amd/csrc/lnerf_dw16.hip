@@ -112,6 +112,8 @@ struct Dw16Args {
     int rpad;                   // slab positions per layer
     const int* eshift;          // per-layer product shift E_l (k1_reduce_kernel)
     int L;
+    const int* gate;            // nullable: the launch exits at once unless *gate != 0 (the floor guard's
+                                // re-run, lnerf_internal.h kGuardExp)
 };
 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
@@ -767,12 +769,12 @@ __device__ __forceinline__ void dw_split(const Dw16Args& a, int l, int sp, unsig
 
     if constexpr (PL == 2 && LNERF_DW16_XROW) {
         const int2 nx = xrow_pass<TI, TJ>(A, G, se, KT, NT, m, hb0, hb1, a0, g0, active, acc, lds, E, xany);
-        if (threadIdx.x == 0) {
+        if (threadIdx.x == 0 && a.xcount) {
             a.xcount[2 * blockIdx.x] = nx.x;
             a.xcount[2 * blockIdx.x + 1] = nx.y;
         }
     } else {
-        if (threadIdx.x == 0) a.xcount[2 * blockIdx.x] = a.xcount[2 * blockIdx.x + 1] = 0;
+        if (threadIdx.x == 0 && a.xcount) a.xcount[2 * blockIdx.x] = a.xcount[2 * blockIdx.x + 1] = 0;
     }
 
     // partial [split][k][j], k < KT*32, j < NT*32 (32x32 C/D layout: row (r&3)+8(r>>2)+4h, col l&31)
@@ -847,6 +849,7 @@ template <int PL>
 __global__ void __launch_bounds__(kThreads, 1) __attribute__((amdgpu_waves_per_eu(kWavesDw / 4, kWavesDw / 4)))
 dw16_kernel(Dw16Args a) {
     __shared__ __attribute__((aligned(16))) unsigned char lds[dw_lds_bytes<PL>()];
+    if (a.gate && *a.gate == 0) return;
     int li = 0;
     while (li + 1 < a.nl && (int)blockIdx.x >= a.wg_off[li + 1]) ++li;
     const int l = a.lid[li], sp = blockIdx.x - a.wg_off[li];
@@ -883,8 +886,9 @@ dw16_kernel(Dw16Args a) {
 __global__ void __launch_bounds__(1024) k1_reduce_kernel(const int* __restrict__ epart, int n,
                                                          int* __restrict__ eshift, int nl,
                                                          const float* __restrict__ loss_part, int nwg,
-                                                         float* total, float* out_loss) {
+                                                         float* total, float* out_loss, const int* gate) {
     __shared__ float red[1024];
+    if (gate && *gate == 0) return;
     const int t = threadIdx.x;
     if ((int)blockIdx.x < nl) {
         const int* q = epart + (size_t)blockIdx.x * n;
@@ -951,6 +955,9 @@ void dw16_launch(const FusedPlan& p, hipStream_t s) {
     a.rpad = p.num_wg * p.tile;
     a.eshift = p.dw_shift;
     a.L = p.L;
+    a.gate = p.gate;
+    // the guard's re-run leaves the primary step's exceptional-row counts (lnerf_ctx_exceptional_rows)
+    if (p.gate) a.xcount = nullptr;
     static_assert(sizeof(Dw16Args) <= 4096, "kernel arguments");
     // the per-layer product shifts of k1_reduce_launch (launched right after k1)
     if (p.x6 == 2) dw16_kernel<2><<<p.dw_grid, kThreads, 0, s>>>(a);
@@ -961,7 +968,7 @@ void dw16_launch(const FusedPlan& p, hipStream_t s) {
 void k1_reduce_launch(const FusedPlan& p, float* out_loss, hipStream_t s) {
     // k1's per-wave minima: tile / 16 waves per workgroup
     k1_reduce_kernel<<<p.L + 1, 1024, 0, s>>>(p.epart, p.num_wg * (p.tile / 16), p.dw_shift, p.L, p.loss_part,
-                                              p.num_wg, p.loss_total, out_loss);
+                                              p.num_wg, p.loss_total, out_loss, p.gate);
 }
 
 }  // namespace lnerf

@@ -85,6 +85,11 @@ struct ReduceArgs {
     float* d_bs;
     const float* scale;          // nullable device scalar (seed = loss)
     int accumulate;
+    // the floor guard (lnerf_internal.h kGuardExp): with gate set, the launch runs only when
+    // (*gate != 0) == gate_want -- the fp16x3 partials' reduction when the guard stayed clear, the
+    // bf16x6 re-run's when it fired
+    const int* gate;
+    int gate_want;
 };
 
 // In-order sum of n strided partials (deterministic); loads are issued 8 at a time so the
@@ -104,6 +109,7 @@ __device__ __forceinline__ float sum_parts(const float* __restrict__ p, size_t s
 }
 
 __global__ void grad_reduce_kernel(ReduceArgs a) {
+    if (a.gate && ((*a.gate != 0) ? 1 : 0) != a.gate_want) return;
     const size_t nW = (size_t)a.L * a.w_k * a.w_n, nB = (size_t)a.L * a.w_n;
     const float sc = a.scale ? *a.scale : 1.0f;
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < nW + nB;
@@ -245,7 +251,7 @@ bool fused_supported(const lnerf_mlp& m, int rays, int S, int input_mode, const 
 static size_t workspace_floats(const lnerf_mlp& m, int rays, int S, bool train, int dw_grid, int tile) {
     Layout y;
     make_layout(y, m, rays, S, train, dw_grid, tile);
-    return align_up(y.act_total, 64) + align_up(y.grad_total, 64) + align_up((size_t)y.num_wg, 64) +
+    return 64 + align_up(y.act_total, 64) + align_up(y.grad_total, 64) + align_up((size_t)y.num_wg, 64) +
            align_up(y.dwp_total, 64) + align_up(y.dbp_total, 64) + 64 + align_up((size_t)kLossStage1, 64) +
            align_up((y.w16_total + 1) / 2, 64) +
            align_up(y.b16_total, 64) + align_up(y.mask_total * 2, 64) + 64 +   // + the fp16x3 shifts
@@ -313,7 +319,9 @@ static void fused_plan_tile(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch&
         off += align_up(floats, 64);
         return q;
     };
-    p.act = take(y.act_total);
+    // every region but the activation slabs (whose size follows the split: a_tile_floats) first, so
+    // that the fp16x3 plan and its bf16x6 re-run (the floor guard) share all other pointers
+    p.guard = (int*)take(64);
     p.grad = take(y.grad_total);
     p.loss_part = take((size_t)y.num_wg);
     p.dw_part = take(y.dwp_total);
@@ -333,6 +341,7 @@ static void fused_plan_tile(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch&
     if (train) off += align_up((size_t)p.L * y.num_wg * 8, 64);
     p.xcount = (int*)(base + off);
     if (train) off += align_up((size_t)2 * y.dw_grid, 64);
+    p.act = take(y.act_total);
 }
 
 void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws_base, int flags, bool train,
@@ -351,21 +360,7 @@ void fused_plan(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch& b, void* ws
     p.head_fit = (flags & LNERF_HEAD_FIT) ? 1 : 0;
 }
 
-void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, const lnerf_batch& b, float seed,
-                      int flags, const lnerf_outputs& out, hipStream_t s, hipEvent_t* ev) {
-    const bool seed_loss = (flags & LNERF_SEED_LOSS) != 0;
-    auto mark = [&](int i) {
-        if (ev) (void)hipEventRecord(ev[i], s);
-    };
-    mark(0);
-    k16_pack(p, ws, bs, s);
-    mark(1);
-    k16_launch(p, b, seed_loss ? 1.0f : seed, out, true, s);
-    mark(2);
-    k1_reduce_launch(p, out.loss, s);
-    mark(3);
-    dw16_launch(p, s);
-    mark(4);
+static ReduceArgs reduce_args(const FusedPlan& p, const lnerf_outputs& out, int flags) {
     ReduceArgs ra{};
     ra.L = p.L;
     for (int l = 0; l < p.L; ++l) {
@@ -383,10 +378,48 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
     ra.db_part = p.db_part;
     ra.d_ws = out.d_ws;
     ra.d_bs = out.d_bs;
-    ra.scale = seed_loss ? p.loss_total : nullptr;
+    ra.scale = (flags & LNERF_SEED_LOSS) ? p.loss_total : nullptr;
     ra.accumulate = (flags & LNERF_ACCUMULATE) ? 1 : 0;
+    return ra;
+}
+
+void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, const lnerf_batch& b, float seed,
+                      int flags, const lnerf_outputs& out, hipStream_t s, hipEvent_t* ev, const FusedPlan* px) {
+    const bool seed_loss = (flags & LNERF_SEED_LOSS) != 0;
+    auto mark = [&](int i) {
+        if (ev) (void)hipEventRecord(ev[i], s);
+    };
     const size_t nred = (size_t)p.L * p.w_k * p.w_n + (size_t)p.L * p.w_n;
-    grad_reduce_kernel<<<(unsigned)((nred + 255) / 256), 256, 0, s>>>(ra);
+    const unsigned rgrid = (unsigned)((nred + 255) / 256);
+    mark(0);
+    k16_pack(p, ws, bs, s);
+    mark(1);
+    k16_launch(p, b, seed_loss ? 1.0f : seed, out, true, s);
+    mark(2);
+    k1_reduce_launch(p, out.loss, s);
+    mark(3);
+    dw16_launch(p, s);
+    mark(4);
+    ReduceArgs ra = reduce_args(p, out, flags);
+    if (px && p.guard) {
+        // the floor guard (lnerf_internal.h kGuardExp): this reduction runs only if k1 left the guard
+        // clear; otherwise the same step again on the bf16x6 split (px: the same workspace, every
+        // pointer but the activation slabs shared), each kernel exiting at once while the guard is
+        // clear, and its reduction in place of this one
+        ra.gate = p.guard;
+        ra.gate_want = 0;
+        grad_reduce_kernel<<<rgrid, 256, 0, s>>>(ra);
+        k16_pack(*px, ws, bs, s);
+        k16_launch(*px, b, seed_loss ? 1.0f : seed, out, true, s);
+        k1_reduce_launch(*px, out.loss, s);
+        dw16_launch(*px, s);
+        ReduceArgs rx = reduce_args(*px, out, flags);
+        rx.gate = p.guard;
+        rx.gate_want = 1;
+        grad_reduce_kernel<<<rgrid, 256, 0, s>>>(rx);
+    } else {
+        grad_reduce_kernel<<<rgrid, 256, 0, s>>>(ra);
+    }
     if (seed_loss) {
         if (out.d_dists) k_scale_by_scalar(out.d_dists, (size_t)p.R, p.loss_total, s);
         if (out.d_target)

@@ -100,7 +100,7 @@ enum : unsigned {
     kKnobK16Prio = 1u << 4, kKnobK16Spread = 1u << 5, kKnobProf = 1u << 6, kKnobA24 = 1u << 7,
     kKnobK16Only = 1u << 8, kKnobDwSplitLate = 1u << 9, kKnobDwDepth = 1u << 10, kKnobDwSwz = 1u << 11,
     kKnobK16Pin = 1u << 12, kKnobK16FdSrc = 1u << 13, kKnobKrStagger = 1u << 15, kKnobDwXrow = 1u << 17,
-    kKnobKrSched = 1u << 18, kKnobDwWaves = 1u << 14, kKnobKrDist = 1u << 19, kKnobPeDoubling = 1u << 20, kKnobK16OneChunk = 1u << 22, kKnobK16WaveComp = 1u << 23, kKnobK16EpiFma = 1u << 24,
+    kKnobGuard = 1u << 25, kKnobK16G2 = 1u << 26, kKnobKrSched = 1u << 18, kKnobDwWaves = 1u << 14, kKnobKrDist = 1u << 19, kKnobPeDoubling = 1u << 20, kKnobK16OneChunk = 1u << 22, kKnobK16WaveComp = 1u << 23, kKnobK16EpiFma = 1u << 24,
 };
 unsigned k16_build_knobs();
 unsigned dw16_build_knobs();
@@ -240,7 +240,30 @@ struct FusedPlan {
     int* xcount;                         // per dW workgroup: exceptional rows it multiplied, of them rays'
                                          // last samples (xrow_pass) [dw_grid][2]
     int* epart;                          // k1's per-wave min of exA + exG [L][num_wg * waves]
+    // the fp16x3 floor guard (kGuardExp): the primary fp16x3 step's k1 sets *guard, its pack zeroes it
+    // first; the bf16x6 re-run's kernels (gate = the same word) exit at once unless it is set
+    int* guard;                          // nullable: no floor test
+    const int* gate;                     // nullable: run unconditionally
 };
+
+// ---- the fp16x3 floor guard (round 6) ----------------------------------------------------------
+// k1's reverse chain splits each G row at the row's own shift (max in [2^13, 2^14)), so an element
+// of a G row that sits below 2^kGuardExp after that shift -- about 2^-37.5 of its row's maximum --
+// has nothing left in either fp16 piece (fp16's smallest subnormal is 2^-24) and is lost from every
+// product and every G row the chain derives from it, which no later exact arithmetic can restore
+// (edge_finite_6x8: rgb adjoints 2^40 below their sample's sigma adjoint, carried by the fixture's
+// permutation weights into a dW column of their own, came out ~0.5 % wrong). k1 tests the head row
+// as its pass splits it (column-scaled) and every hidden G row it produces (G_{L-2} .. G_0) against
+// that floor; a step where any element fails is re-run on the bf16x6 split (fp32's exponent range per
+// element) before the dW/db reduction, on the device, without a host round trip (fused_train_step).
+// The default precision only (an explicit LNERF_MFMA_F16X3 asks for fp16x3 exactly). On the cfg3
+// bench batch the smallest G element sits at 2^-16.1 after its row's shift (hidden rows) and 2^-4.7
+// (head rows; scripts/xcheck_study.py), eight binades and more above the floor.
+constexpr int kGuardExp = -24;
+// GUARD: A/B knob (0: no floor test in k1 and no gated re-run; the round-5 behaviour)
+#ifndef LNERF_GUARD
+#define LNERF_GUARD 1
+#endif
 
 bool fused_supported(const lnerf_mlp& mlp, int rays, int S, int input_mode, const char** why,
                      bool head_fit = false);
@@ -251,9 +274,11 @@ size_t fused_workspace_bytes(const lnerf_mlp& mlp, int rays, int S, bool train =
 void fused_plan(FusedPlan& p, const lnerf_mlp& mlp, const lnerf_batch& b, void* ws_base, int flags,
                 bool train = true, int dw_grid = 0);
 // ev: nullable array of 7 events recorded between the step's kernels (LNERF_TIMING)
+// px (nullable): the bf16x6 plan of the same batch on the same workspace, run gated on p.guard (the
+// fp16x3 floor guard, kGuardExp)
 void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, const lnerf_batch& b,
                       float seed, int flags, const lnerf_outputs& out, hipStream_t s,
-                      hipEvent_t* ev);
+                      hipEvent_t* ev, const FusedPlan* px = nullptr);
 // ev: nullable array of events as fused_train_step's ([1]-[2] bracket the forward kernel)
 void fused_render(const FusedPlan& p, const float* ws, const float* bs, const lnerf_batch& b,
                   const lnerf_outputs& out, hipStream_t s, int flags, hipEvent_t* ev);

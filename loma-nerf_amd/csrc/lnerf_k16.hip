@@ -59,15 +59,19 @@ constexpr int kCompBytes = 2688 * 4;          // composite_tile's scratch (comp[
 //    chunk apart; the ring then needs 3 slots (the late waves still read the previous chunk
 //    while every wave reads the current one and the next one lands).
 //  * NW = 4 (two workgroups per CU, each within 80 KiB of LDS): KC = 1, two 32 KiB slots.
-template <int PL, int NW = 8>
+//  * NG = 2 (two 16-sample groups per wave, NW = 4: one wave per SIMD, a 128-sample tile): every
+//    weight fragment read from LDS feeds both groups' MFMAs; the ring as NW = 8 (KC = 2, two 64 KiB
+//    slots), 16 pieces per wave per chunk.
+template <int PL, int NW = 8, int NG = 1>
 struct Ring {
-    static constexpr int KC = (PL == 3 || NW == 4) ? 1 : 2;
+    static constexpr int KC = (PL == 3 || (NW == 4 && NG == 1)) ? 1 : 2;
     static constexpr bool stagger = PL == 3 && NW == 8;
     static constexpr int slots = stagger ? 3 : 2;
     static constexpr int slot_bytes = KC * kMaxT * PL * 1024;
+    static constexpr int pieces = slot_bytes / (NW * 1024);   // per wave, a whole chunk
     static constexpr int off_comp = slots * slot_bytes;
     static constexpr int off_ray = off_comp + kCompBytes;
-    static constexpr int off_bias = off_ray + 16 * NW * 4;
+    static constexpr int off_bias = off_ray + 16 * NW * NG * 4;
     static constexpr int lds_bytes = off_bias + 3 * 256 * 4;   // + a 3-slot ring of layer biases
     static_assert(lds_bytes + 1024 <= 160 * 1024, "LDS budget (+1 KiB for the profiling build)");
     static_assert((KC * kMaxT - 1) * PL * 1024 < 65536, "ds_read offsets are 16-bit immediates");
@@ -114,6 +118,8 @@ struct K16Args {
     int* epart;        // training: per-wave min over samples of exA + exG, [l][num_wg * 8]
     int head_fit;      // the mlp_fit head (comp::fit_tile) instead of the NeRF compositing
     int nout;          // head outputs (the mlp_fit head's width)
+    int* guard;        // PL = 2 training, nullable: set when a hidden G row fails the floor (kGuardExp)
+    const int* gate;   // nullable: the launch exits at once unless *gate != 0 (the guard's re-run)
 };
 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
@@ -226,6 +232,7 @@ __device__ __forceinline__ void dma_barrier(int pending) {
     if (pending == 0) vm_wait<0>();
     else if (pending == 2) vm_wait<2>();
     else if (pending == 4) vm_wait<4>();
+    else if (pending == 8) vm_wait<8>();
     else if (pending > 0) vm_wait_n(pending, std::make_integer_sequence<int, 64>{});
     PROF_ADD(kPfVm, t0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -379,10 +386,15 @@ __device__ __forceinline__ void read_tile(const unsigned char* base, bf8 (&w)[3]
 #define LNERF_K16_ONECHUNK 1
 #endif
 // k-steps per chunk of a pass with NTO output tiles (k16_launch's chunk table follows the same rule)
-template <int NTO, int PL, int NW>
+template <int NTO, int PL, int NW, int NG = 1>
 constexpr int pass_kc() {
-    return (LNERF_K16_ONECHUNK && NTO == 1) ? 8 : Ring<PL, NW>::KC;
+    return (LNERF_K16_ONECHUNK && NTO == 1) ? 8 : Ring<PL, NW, NG>::KC;
 }
+// G2: k1 on two 16-sample groups per wave at one wave per SIMD (k16_fwd_bwd_kernel<16, 2, 4, 2>), every
+// weight fragment feeding both groups' MFMAs (round 6 A/B)
+#ifndef LNERF_K16_G2
+#define LNERF_K16_G2 0
+#endif
 // EPIFMA: the forward epilogue's unscale and bias as one fma (round 5, in-process A/B: k1
 // 1.279 -> 1.261 ms; round 4's bench-level A/B had called it neutral)
 #ifndef LNERF_K16_EPIFMA
@@ -393,7 +405,7 @@ constexpr int pass_kc() {
 #ifndef LNERF_K16_WAVECOMP
 #define LNERF_K16_WAVECOMP 1
 #endif
-constexpr int kPiecesMax = 8;   // pieces per wave of a full chunk (64 KiB / 8 waves, 32 KiB / 4)
+constexpr int kPiecesMax = 8;   // pieces per wave of a full chunk (64 KiB / 8 waves, 32 KiB / 4; NG = 2: 16)
 struct DmaJob {
     const char* src = nullptr;   // the wave's (uniform) address of piece 0
     unsigned char* dst = nullptr;   // LDS address of this wave's piece 0
@@ -408,7 +420,8 @@ __device__ __forceinline__ void dma_piece(const DmaJob& j, int p) {
 // FULL: the chunk is known to be whole (every wave issues kPiecesMax pieces, no per-piece test)
 template <int NTO, int O, int NW, bool FULL, int... P>
 __device__ __forceinline__ void dma_pieces_at(const DmaJob& j, std::integer_sequence<int, P...>) {
-    (((P * NTO) / kPiecesMax == O ? ((FULL || P < j.n) ? dma_piece<NW>(j, P) : void()) : void()), ...);
+    constexpr int KP = sizeof...(P);
+    (((P * NTO) / KP == O ? ((FULL || P < j.n) ? dma_piece<NW>(j, P) : void()) : void()), ...);
 }
 
 // Output tile O of one k-step: issue the reads of tile O + kDist, the MFMAs of tile O (small
@@ -437,44 +450,49 @@ struct NoFill {
 
 // FDP: how this k-step issues the next chunk's DMA: 0 generic (per-piece tests), 3 a whole chunk's
 // 8 pieces (round 5: spreading them over both k-steps of the chunk measured +0.3 % in k1)
-template <int NTO, int PL, int NW, int FDP, int O, typename F = NoFill>
-__device__ __forceinline__ void tile_step(const unsigned char* base, bf8 (&w)[kDist + 1][3], const bf8& bh,
-                                          const bf8& bm, const bf8& bl, fx4 (&out)[kMaxT], const DmaJob& job,
-                                          F& fill) {
+template <int NTO, int PL, int NW, int NG, int FDP, int O, typename F = NoFill>
+__device__ __forceinline__ void tile_step(const unsigned char* base, bf8 (&w)[kDist + 1][3], const bf8 (&bh)[NG],
+                                          const bf8 (&bm)[NG], const bf8 (&bl)[NG], fx4 (&out)[NG][kMaxT],
+                                          const DmaJob& job, F& fill) {
+    constexpr int KP = Ring<PL, NW, NG>::pieces < kPiecesMax ? kPiecesMax : Ring<PL, NW, NG>::pieces;
     if constexpr (O + kDist < NTO) read_tile<PL, O + kDist>(base, w[(O + kDist) % (kDist + 1)]);
-    if constexpr (FDP == 3) dma_pieces_at<NTO, O, NW, true>(job, std::make_integer_sequence<int, kPiecesMax>{});
-    else if (job.n) dma_pieces_at<NTO, O, NW, false>(job, std::make_integer_sequence<int, kPiecesMax>{});
+    if constexpr (FDP == 3) dma_pieces_at<NTO, O, NW, true>(job, std::make_integer_sequence<int, KP>{});
+    else if (job.n) dma_pieces_at<NTO, O, NW, false>(job, std::make_integer_sequence<int, KP>{});
     // keep tile O + kDist's reads ahead of tile O's MFMAs: the machine scheduler otherwise sinks
     // each read next to its first consumer (one MFMA of slack, an LDS round trip exposed per tile);
     // the compiler still places every wait itself
     if constexpr (LNERF_K16_SCHED) __builtin_amdgcn_sched_barrier(0);
     bf8(&c)[3] = w[O % (kDist + 1)];
-    fx4 acc = out[O];
-    if constexpr (PL == 2) {
-        // fp16x3: small terms first (w_hi x_lo, w_lo x_hi), then w_hi x_hi; (bh, bm) = (x_hi, x_lo)
-        acc = mfma16h(c[0], bm, acc);
-        acc = mfma16h(c[1], bh, acc);
-        acc = mfma16h(c[0], bh, acc);
-    } else if constexpr (PL == 3) {
-        acc = mfma16(c[0], bl, acc);
-        acc = mfma16(c[1], bm, acc);
-        acc = mfma16(c[2], bh, acc);
-        acc = mfma16(c[1], bh, acc);
-        acc = mfma16(c[0], bm, acc);
-        acc = mfma16(c[0], bh, acc);
-    } else {
-        acc = mfma16(c[0], bh, acc);
+    // every group's products from the same fragments (NG = 2: half the LDS bytes per MFMA)
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+        fx4 acc = out[q][O];
+        if constexpr (PL == 2) {
+            // fp16x3: small terms first (w_hi x_lo, w_lo x_hi), then w_hi x_hi; (bh, bm) = (x_hi, x_lo)
+            acc = mfma16h(c[0], bm[q], acc);
+            acc = mfma16h(c[1], bh[q], acc);
+            acc = mfma16h(c[0], bh[q], acc);
+        } else if constexpr (PL == 3) {
+            acc = mfma16(c[0], bl[q], acc);
+            acc = mfma16(c[1], bm[q], acc);
+            acc = mfma16(c[2], bh[q], acc);
+            acc = mfma16(c[1], bh[q], acc);
+            acc = mfma16(c[0], bm[q], acc);
+            acc = mfma16(c[0], bh[q], acc);
+        } else {
+            acc = mfma16(c[0], bh[q], acc);
+        }
+        out[q][O] = acc;
     }
-    out[O] = acc;
     fill.template at<O>();
 }
 
 // tiles B, B+1, ... of one k-step
-template <int NTO, int PL, int NW, int FDP, int B, typename F, int... O>
+template <int NTO, int PL, int NW, int NG, int FDP, int B, typename F, int... O>
 __device__ __forceinline__ void tile_steps(std::integer_sequence<int, O...>, const unsigned char* base,
-                                           bf8 (&w)[kDist + 1][3], const bf8& bh, const bf8& bm,
-                                           const bf8& bl, fx4 (&out)[kMaxT], const DmaJob& job, F& fill) {
-    (tile_step<NTO, PL, NW, FDP, B + O>(base, w, bh, bm, bl, out, job, fill), ...);
+                                           bf8 (&w)[kDist + 1][3], const bf8 (&bh)[NG], const bf8 (&bm)[NG],
+                                           const bf8 (&bl)[NG], fx4 (&out)[NG][kMaxT], const DmaJob& job, F& fill) {
+    (tile_step<NTO, PL, NW, NG, FDP, B + O>(base, w, bh, bm, bl, out, job, fill), ...);
 }
 
 // LNERF_K16_PIN = 2 (fp16x3, 16 output tiles): the next k-step's operand split and this k-step's
@@ -482,35 +500,40 @@ __device__ __forceinline__ void tile_steps(std::integer_sequence<int, O...>, con
 // tile's MFMAs (pair q of the split after tile 2q + 1, the two 12-B packs after tiles 9 and 11),
 // each result pinned there (in place, no instruction) so the compiler cannot sink it back to the
 // k-step boundary
+template <int NG>
 struct FillSpread {
-    const fx4* in;        // the pass input (in[2 sn], in[2 sn + 1]: the next k-step's features)
+    const fx4 (*in)[kMaxT];   // the pass input per group (in[q][2 sn], in[q][2 sn + 1]: the next k-step's features)
     int sn;               // the next k-step
     bool split;           // there is a next k-step
-    float sc;             // 2^ex
-    unsigned hv[4], lv[4];
+    float sc[NG];         // 2^ex per group
+    unsigned hv[NG][4], lv[NG][4];
     bool pack;            // this k-step's int24 slab values are packed (stored after the last tile)
-    int s, ex;
-    Packed24 pk;
+    int s, ex[NG];
+    Packed24 pk[NG];
+    // group q's split pair k after tile 2 k + 1 + q, its two 12-B packs after tiles 9 + q and 11 + q
     template <int O>
     __device__ __forceinline__ void at() {
-        if constexpr (O == 1 || O == 3 || O == 5 || O == 7) {
-            constexpr int q = (O - 1) / 2;
-            if (split) {
-                const fx4& t = in[2 * sn + (q >> 1)];
-                split_h2(t[2 * (q & 1)], t[2 * (q & 1) + 1], sc, hv[q], lv[q]);
-                pin(hv[q]);
-                pin(lv[q]);
+#pragma unroll
+        for (int q = 0; q < NG; ++q) {
+            if constexpr (O >= 1 && O <= 7 + NG - 1) {
+                if ((O - 1 - q) >= 0 && (O - 1 - q) % 2 == 0 && (O - 1 - q) / 2 < 4) {
+                    const int k = (O - 1 - q) / 2;
+                    if (split) {
+                        const fx4& t = in[q][2 * sn + (k >> 1)];
+                        split_h2(t[2 * (k & 1)], t[2 * (k & 1) + 1], sc[q], hv[q][k], lv[q][k]);
+                        pin(hv[q][k]);
+                        pin(lv[q][k]);
+                    }
+                }
             }
-        }
-        if constexpr (O == 9 || O == 11) {
-            if (pack) {
-                const Packed24 p = pack_slab_step24(in[2 * s], in[2 * s + 1], ex);
-                if constexpr (O == 9) {
-                    pk.p0 = p.p0;
-                    pin(pk.p0);
+            if (pack && (O == 9 + q || O == 11 + q)) {
+                const Packed24 p = pack_slab_step24(in[q][2 * s], in[q][2 * s + 1], ex[q]);
+                if (O == 9 + q) {
+                    pk[q].p0 = p.p0;
+                    pin(pk[q].p0);
                 } else {
-                    pk.p1 = p.p1;
-                    pin(pk.p1);
+                    pk[q].p1 = p.p1;
+                    pin(pk[q].p1);
                 }
             }
         }
@@ -560,25 +583,27 @@ __device__ __forceinline__ void make_b(const fx4 (&in)[kMaxT], int s, int ex, bf
 // (the A_{l-1} or G_l slab of this wave's half-block).
 // FD: this k-step issues the DMA of a chunk known to be whole (the next chunk of the same full
 // pass): kPiecesMax pieces per wave with no per-piece test and no byte arithmetic.
-template <int NTO, int PL, int NW, int FDP = 0, bool A24 = false>
+template <int NTO, int PL, int NW, int NG, int FDP = 0, bool A24 = false>
 __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk, bool last, int& ci,
-                                         unsigned char* ring, float* bias_ring, const fx4 (&in)[kMaxT],
-                                         fx4 (&out)[kMaxT], float* __restrict__ slab, int ex, bf8& bh,
-                                         bf8& bm, bf8& bl, int& pending, const unsigned short* fdsrc) {
-    using R = Ring<PL, NW>;
+                                         unsigned char* ring, float* bias_ring, const fx4 (&in)[NG][kMaxT],
+                                         fx4 (&out)[NG][kMaxT], float* const (&slab)[NG], const int (&ex)[NG],
+                                         bf8 (&bh)[NG], bf8 (&bm)[NG], bf8 (&bl)[NG], int& pending,
+                                         const unsigned short* fdsrc) {
+    using R = Ring<PL, NW, NG>;
     constexpr int KC_BYTES = R::KC * NTO * PL * 1024;
+    constexpr int KP = R::pieces < kPiecesMax ? kPiecesMax : R::pieces;
     const int lane = threadIdx.x & 63;
     const unsigned char* base = ring + (ci % R::slots) * R::slot_bytes + kk * NTO * PL * 1024 + lane * 16;
-    const bool st = slab != nullptr;
+    const bool st = slab[0] != nullptr;
     constexpr bool spread = LNERF_K16_SPREAD && !R::stagger;
     constexpr bool FD = FDP != 0;
     DmaJob job;
     if (kk == 0) {
         // DMA of chunk ci + 1 (its table entry is a scalar load the compiler waits for with
         // lgkmcnt(0), so it is read before the fragment reads are issued). Unspread: every piece
-        // now, before the first weight tiles; spread: one piece per kPiecesMax-th of the output
+        // now, before the first weight tiles; spread: one piece per KP-th of the output
         // tiles, between the MFMAs. The barrier waits for this wave's pieces of chunk ci + 1 only:
-        // the slab stores issued after them (two per k-step) stay in flight.
+        // the slab stores issued after them (two per k-step and group) stay in flight.
         // FDSRC: the next chunk of this full pass, whole, no biases (fdsrc = its source)
         const ChunkT c = (FD && LNERF_K16_FDSRC) ? ChunkT{fdsrc, KC_BYTES, -1} : chunk_at(a, ci + 1);
         unsigned char* dst = ring + ((ci + 1) % R::slots) * R::slot_bytes;
@@ -586,7 +611,7 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
         if constexpr (spread) {
             const int wave = wave_id();
             const int woff = wave * 1024;
-            job.n = FD ? kPiecesMax
+            job.n = FD ? KP
                        : (c.src && woff < c.bytes) ? (c.bytes - woff + NW * 1024 - 1) / (NW * 1024) : 0;
             job.src = (const char*)c.src + woff;
             job.dst = dst + woff;
@@ -602,7 +627,7 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
         asm volatile("" ::: "memory");   // the slab stores stay younger than the pieces
         pending = issued ? 0 : -1;
     }
-    if (st && pending >= 0) pending += 2;
+    if (st && pending >= 0) pending += 2 * NG;
     const bool late = R::stagger && wave_id() >= 4;
     bf8 w[kDist + 1][3];
     read_tile<PL, 0>(base, w[0]);
@@ -610,10 +635,13 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
     if constexpr (NTO > 2 && kDist > 2) read_tile<PL, 2>(base, w[2]);
     static_assert(kDist == 2 || kDist == 3, "the prologue reads kDist tiles");
     auto store = [&]() {
-        if constexpr (A24) {
-            store_slab_step24((unsigned char*)slab + s * 3072, in[2 * s], in[2 * s + 1], ex);
-        } else {
-            store_slab_step(slab + s * 1024, in[2 * s], in[2 * s + 1]);
+#pragma unroll
+        for (int q = 0; q < NG; ++q) {
+            if constexpr (A24) {
+                store_slab_step24((unsigned char*)slab[q] + s * 3072, in[q][2 * s], in[q][2 * s + 1], ex[q]);
+            } else {
+                store_slab_step(slab[q] + s * 1024, in[q][2 * s], in[q][2 * s + 1]);
+            }
         }
     };
     if (st && !spread) store();
@@ -623,116 +651,141 @@ __device__ __forceinline__ void k16_step(const K16Args& a, int ks, int s, int kk
     constexpr int H = half_tiles<NTO>();   // split after tile H
     constexpr bool spread_fill = LNERF_K16_PIN == 2 && PL == 2 && NTO == 16 && !R::stagger;
     // a late wave meets the barrier before this k-step's spread slab stores: they are not pending yet
-    const int late_pending = (st && spread && pending >= 2) ? pending - 2 : pending;
+    const int late_pending = (st && spread && pending >= 2 * NG) ? pending - 2 * NG : pending;
     if constexpr (spread_fill) {
-        FillSpread f;
+        FillSpread<NG> f;
         f.in = in;
         f.sn = s + 1 < 8 ? s + 1 : 0;
         f.split = s + 1 < ks;
-        f.sc = __builtin_ldexpf(1.0f, ex);
+#pragma unroll
+        for (int q = 0; q < NG; ++q) {
+            f.sc[q] = __builtin_ldexpf(1.0f, ex[q]);
+            f.ex[q] = ex[q];
+        }
         f.pack = A24 && st && spread;
         f.s = s;
-        f.ex = ex;
-        tile_steps<NTO, PL, NW, FDP, 0>(std::make_integer_sequence<int, H>{}, base, w, bh, bm, bl, out, job, f);
+        tile_steps<NTO, PL, NW, NG, FDP, 0>(std::make_integer_sequence<int, H>{}, base, w, bh, bm, bl, out, job, f);
         if (late && last) dma_barrier(late_pending);
-        tile_steps<NTO, PL, NW, FDP, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, bh, bm, bl, out, job, f);
+        tile_steps<NTO, PL, NW, NG, FDP, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, bh, bm, bl, out, job,
+                                            f);
         if (st && spread) {
             asm volatile("" ::: "memory");
-            if constexpr (A24) store_packed24((unsigned char*)slab + s * 3072, f.pk);
-            else store_slab_step(slab + s * 1024, in[2 * s], in[2 * s + 1]);
+#pragma unroll
+            for (int q = 0; q < NG; ++q) {
+                if constexpr (A24) store_packed24((unsigned char*)slab[q] + s * 3072, f.pk[q]);
+                else store_slab_step(slab[q] + s * 1024, in[q][2 * s], in[q][2 * s + 1]);
+            }
         }
         if (!late && last) dma_barrier(pending);
         if (last) ++ci;
         typedef unsigned u4 __attribute__((ext_vector_type(4)));
-        bh = f.split ? __builtin_bit_cast(bf8, u4{f.hv[0], f.hv[1], f.hv[2], f.hv[3]}) : bf8{};
-        bm = f.split ? __builtin_bit_cast(bf8, u4{f.lv[0], f.lv[1], f.lv[2], f.lv[3]}) : bf8{};
+#pragma unroll
+        for (int q = 0; q < NG; ++q) {
+            bh[q] = f.split ? __builtin_bit_cast(bf8, u4{f.hv[q][0], f.hv[q][1], f.hv[q][2], f.hv[q][3]}) : bf8{};
+            bm[q] = f.split ? __builtin_bit_cast(bf8, u4{f.lv[q][0], f.lv[q][1], f.lv[q][2], f.lv[q][3]}) : bf8{};
+        }
         return;
     }
     NoFill nf;
-    tile_steps<NTO, PL, NW, FDP, 0>(std::make_integer_sequence<int, H>{}, base, w, bh, bm, bl, out, job, nf);
-    if constexpr (R::stagger) mfma_branch_guard(out[H > 0 ? H - 1 : 0]);
+    tile_steps<NTO, PL, NW, NG, FDP, 0>(std::make_integer_sequence<int, H>{}, base, w, bh, bm, bl, out, job, nf);
+    if constexpr (R::stagger) mfma_branch_guard(out[0][H > 0 ? H - 1 : 0]);
     if (late && last) dma_barrier(late_pending);
-    bf8 nh = {}, nm = {}, nl = {};
-    if (s + 1 < ks) make_b<PL>(in, s + 1 < 8 ? s + 1 : 0, ex, nh, nm, nl);
-    tile_steps<NTO, PL, NW, FDP, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, bh, bm, bl, out, job, nf);
+    bf8 nh[NG] = {}, nm[NG] = {}, nl[NG] = {};
+    if (s + 1 < ks) {
+#pragma unroll
+        for (int q = 0; q < NG; ++q) make_b<PL>(in[q], s + 1 < 8 ? s + 1 : 0, ex[q], nh[q], nm[q], nl[q]);
+    }
+    tile_steps<NTO, PL, NW, NG, FDP, H>(std::make_integer_sequence<int, NTO - H>{}, base, w, bh, bm, bl, out, job, nf);
     if (st && spread) {
         asm volatile("" ::: "memory");
         store();
     }
-    if constexpr (R::stagger) mfma_branch_guard(out[NTO - 1]);
+    if constexpr (R::stagger) mfma_branch_guard(out[0][NTO - 1]);
     if (!late && last) dma_barrier(pending);
     if (last) ++ci;
-    bh = nh;
-    bm = nm;
-    bl = nl;
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+        bh[q] = nh[q];
+        bm[q] = nm[q];
+        bl[q] = nl[q];
+    }
 }
 
 // One k-step S of a pass. FULL: the pass has all 8 k-steps (a 256-wide input), so the step
 // bounds are compile-time and, where the chunk after this one belongs to the same pass and is
 // whole (KC NTO PL KiB = kPiecesMax pieces per wave), its DMA is issued without per-piece tests.
-template <int NTO, int PL, int NW, bool FULL, bool A24, int S>
+template <int NTO, int PL, int NW, int NG, bool FULL, bool A24, int S>
 __device__ __forceinline__ void k16_pass_step(const K16Args& a, int ks, int& ci, unsigned char* ring,
-                                              float* bias_ring, const fx4 (&in)[kMaxT], fx4 (&out)[kMaxT],
-                                              float* __restrict__ slab, int ex, bf8& bh, bf8& bm, bf8& bl,
-                                              int& pending, const unsigned short* pbase) {
-    constexpr int KC = pass_kc<NTO, PL, NW>();
+                                              float* bias_ring, const fx4 (&in)[NG][kMaxT], fx4 (&out)[NG][kMaxT],
+                                              float* const (&slab)[NG], const int (&ex)[NG], bf8 (&bh)[NG],
+                                              bf8 (&bm)[NG], bf8 (&bl)[NG], int& pending,
+                                              const unsigned short* pbase) {
+    constexpr int KC = pass_kc<NTO, PL, NW, NG>();
+    using R = Ring<PL, NW, NG>;
     if (FULL || S < ks) {
         constexpr int kk = S % KC;
         const bool last = kk == KC - 1 || (FULL ? S == 7 : S + 1 == ks);
+        // (a whole chunk is exactly KP pieces per wave: KP = 8, or 16 for NG = 2)
+        constexpr int KP = R::pieces < kPiecesMax ? kPiecesMax : R::pieces;
         constexpr bool whole_next = LNERF_K16_FULLDMA && FULL && S / KC + 1 < 8 / KC &&
-                                    KC * NTO * PL == kPiecesMax * NW && LNERF_K16_SPREAD && !Ring<PL, NW>::stagger;
+                                    KC * NTO * PL == KP * NW && LNERF_K16_SPREAD && !R::stagger;
         constexpr int fd = whole_next && kk == 0 ? 3 : 0;
         // the source of the chunk after this one (S / KC + 1 of the pass), for FDSRC
         const unsigned short* fdsrc = pbase + (size_t)(S / KC + 1) * (KC * NTO * PL * 512);
-        k16_step<NTO, PL, NW, fd, A24>(a, FULL ? 8 : ks, S, kk, last, ci, ring, bias_ring, in, out, slab, ex, bh,
-                                       bm, bl, pending, fdsrc);
+        k16_step<NTO, PL, NW, NG, fd, A24>(a, FULL ? 8 : ks, S, kk, last, ci, ring, bias_ring, in, out, slab, ex,
+                                           bh, bm, bl, pending, fdsrc);
     }
 }
-template <int NTO, int PL, int NW, bool FULL, bool A24, int... S>
+template <int NTO, int PL, int NW, int NG, bool FULL, bool A24, int... S>
 __device__ __forceinline__ void k16_pass_steps(std::integer_sequence<int, S...>, const K16Args& a, int ks, int& ci,
-                                               unsigned char* ring, float* bias_ring, const fx4 (&in)[kMaxT],
-                                               fx4 (&out)[kMaxT], float* __restrict__ slab, int ex, bf8& bh,
-                                               bf8& bm, bf8& bl, int& pending, const unsigned short* pbase) {
-    (k16_pass_step<NTO, PL, NW, FULL, A24, S>(a, ks, ci, ring, bias_ring, in, out, slab, ex, bh, bm, bl, pending,
-                                              pbase), ...);
+                                               unsigned char* ring, float* bias_ring, const fx4 (&in)[NG][kMaxT],
+                                               fx4 (&out)[NG][kMaxT], float* const (&slab)[NG], const int (&ex)[NG],
+                                               bf8 (&bh)[NG], bf8 (&bm)[NG], bf8 (&bl)[NG], int& pending,
+                                               const unsigned short* pbase) {
+    (k16_pass_step<NTO, PL, NW, NG, FULL, A24, S>(a, ks, ci, ring, bias_ring, in, out, slab, ex, bh, bm, bl, pending,
+                                                  pbase), ...);
 }
 
-// One pass (a layer's forward or backward MMA) over its ks k-steps, Ring::KC k-steps per chunk.
+// One pass (a layer's forward or backward MMA) over its ks k-steps, Ring::KC k-steps per chunk, for
+// the wave's NG sample groups (each its own input, accumulators, slab and shift).
 // A24: the pass's input slab (a forward pass's A_{l-1}) is int24 (store_slab_step24).
 // pbase: the pass's first chunk in w16 (FULL passes with FDSRC; otherwise unused)
-template <int NTO, int PL, int NW, bool FULL = false, bool A24 = false>
+template <int NTO, int PL, int NW, int NG, bool FULL = false, bool A24 = false>
 __device__ __forceinline__ void k16_pass(const K16Args& a, int ks, int& ci, unsigned char* ring,
-                                         float* bias_ring, const fx4 (&in)[kMaxT], fx4 (&out)[kMaxT],
-                                         float* __restrict__ slab, int ex = 0, const unsigned short* pbase = nullptr) {
-    bf8 bh = {}, bm = {}, bl = {};
-    make_b<PL>(in, 0, ex, bh, bm, bl);
+                                         float* bias_ring, const fx4 (&in)[NG][kMaxT], fx4 (&out)[NG][kMaxT],
+                                         float* const (&slab)[NG], const int (&ex)[NG],
+                                         const unsigned short* pbase = nullptr) {
+    bf8 bh[NG] = {}, bm[NG] = {}, bl[NG] = {};
+#pragma unroll
+    for (int q = 0; q < NG; ++q) make_b<PL>(in[q], 0, ex[q], bh[q], bm[q], bl[q]);
     int pending = 0;
-    k16_pass_steps<NTO, PL, NW, FULL, A24>(std::make_integer_sequence<int, 8>{}, a, ks, ci, ring, bias_ring, in, out,
-                                           slab, ex, bh, bm, bl, pending, pbase);
+    k16_pass_steps<NTO, PL, NW, NG, FULL, A24>(std::make_integer_sequence<int, 8>{}, a, ks, ci, ring, bias_ring, in,
+                                               out, slab, ex, bh, bm, bl, pending, pbase);
 }
 // a hidden layer's pass: the FULL instantiation for 256-wide inputs (every hidden layer of cfg3)
-template <int HT, int PL, int NW, bool A24 = false>
+template <int HT, int PL, int NW, int NG, bool A24 = false>
 __device__ __forceinline__ void k16_hidden_pass(const K16Args& a, int ks, int& ci, unsigned char* ring,
-                                                float* bias_ring, const fx4 (&in)[kMaxT], fx4 (&out)[kMaxT],
-                                                float* __restrict__ slab, int ex, const unsigned short* pbase) {
+                                                float* bias_ring, const fx4 (&in)[NG][kMaxT], fx4 (&out)[NG][kMaxT],
+                                                float* const (&slab)[NG], const int (&ex)[NG],
+                                                const unsigned short* pbase) {
     if constexpr (LNERF_K16_FULLDMA && HT == 16) {
         if (ks == 8) {
-            k16_pass<HT, PL, NW, true, A24>(a, ks, ci, ring, bias_ring, in, out, slab, ex, pbase);
+            k16_pass<HT, PL, NW, NG, true, A24>(a, ks, ci, ring, bias_ring, in, out, slab, ex, pbase);
             return;
         }
     }
-    k16_pass<HT, PL, NW, false, A24>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
+    k16_pass<HT, PL, NW, NG, false, A24>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
 }
 
-template <int PL, int NW>
+template <int PL, int NW, int NG>
 __device__ __forceinline__ void k16_pass_n(const K16Args& a, int ks, int& ci, unsigned char* ring,
-                                           float* bias_ring, int nto, const fx4 (&in)[kMaxT],
-                                           fx4 (&out)[kMaxT], float* slab, int ex) {
-    if (nto <= 1) k16_pass<1, PL, NW>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
-    else if (nto <= 2) k16_pass<2, PL, NW>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
-    else if (nto <= 4) k16_pass<4, PL, NW>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
-    else if (nto <= 8) k16_pass<8, PL, NW>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
-    else k16_pass<16, PL, NW>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
+                                           float* bias_ring, int nto, const fx4 (&in)[NG][kMaxT],
+                                           fx4 (&out)[NG][kMaxT], float* const (&slab)[NG], const int (&ex)[NG]) {
+    if (nto <= 1) k16_pass<1, PL, NW, NG>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
+    else if (nto <= 2) k16_pass<2, PL, NW, NG>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
+    else if (nto <= 4) k16_pass<4, PL, NW, NG>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
+    else if (nto <= 8) k16_pass<8, PL, NW, NG>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
+    else k16_pass<16, PL, NW, NG>(a, ks, ci, ring, bias_ring, in, out, slab, ex);
 }
 
 // The per-sample max|x| of a pass's input (lanes n, n + 16, n + 32, n + 48 hold sample n's
@@ -762,14 +815,14 @@ __device__ __forceinline__ int shift_of(float m) { return fp16x3_shift(m); }
 // row of layer l (byte 0 of its word); which = 1: the G_l row, with the row's exceptional-row bound
 // dmax (bytes 2, 3). Issued before the pass's first DMA, so it is older than every piece a
 // dma_barrier waits for. Returns the shift.
-__device__ __forceinline__ int store_sexp(const K16Args& a, int l, int which, float m, int dmax = 0) {
+__device__ __forceinline__ int store_sexp(const K16Args& a, int l, int which, float m, int dmax, int lw, int nlw) {
     const int lane = threadIdx.x & 63;
     // -128: an all-zero row; -127 (activation rows only): a row with a non-finite value, int24-encoded
     // at shift 0, whose NaN / infinity codes dw16 turns back into NaN (kSexpNonFinite)
     const bool fin = m < __builtin_inff();
     const int x = (m > 0.0f && fin) ? shift_of(m) : (which == 0 && !(m == 0.0f)) ? kSexpNonFinite : -128;
     if (lane < 16) {
-        const int p = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + lane;
+        const int p = (blockIdx.x * nlw + lw) * 16 + lane;   // lw: the 16-sample group's logical wave
         unsigned char* w = a.sexp + ((size_t)l * a.rpad + p) * 4;
         if (which == 0) *w = (unsigned char)x;
         else *(unsigned short*)(w + 2) = (unsigned short)((x & 0xFF) | ((dmax & 0xFF) << 8));
@@ -800,12 +853,12 @@ struct ExPack {
 // marked -128 excluded, and every ray's last sample, which dw16 multiplies on the bf16x6 split
 // whenever its products exceed E_l: lnerf_internal.h kXrowLast), one plain store per wave into
 // epart[l][global wave]; k1_reduce_kernel folds them into dw16's per-layer product shift E_l.
-__device__ __forceinline__ void store_emin(const K16Args& a, int l, int xa, int xg, bool excluded) {
+__device__ __forceinline__ void store_emin(const K16Args& a, int l, int xa, int xg, bool excluded, int lw, int nlw) {
     int v = (xa < -126 || xg < -126 || excluded) ? (1 << 20) : xa + xg;
 #pragma unroll
     for (int d = 1; d < 16; d <<= 1) v = min(v, __shfl_xor(v, d));
     if ((threadIdx.x & 63) == 0)
-        a.epart[((size_t)l * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)] = v;
+        a.epart[((size_t)l * gridDim.x + blockIdx.x) * nlw + lw] = v;
 }
 
 // The layer's biases in the accumulator layout (fx4 = 4 consecutive features of a lane group),
@@ -841,6 +894,15 @@ __device__ __forceinline__ void head_bscale(const K16Args& a, fx4 (&act)[kMaxT])
     for (int i = 0; i < 4; ++i) act[0][i] = __builtin_ldexpf(act[0][i], ew - head_col_shift(a.hexp[4 * g + i], lm));
 }
 
+// the floor guard (lnerf_internal.h kGuardExp): the smallest frexp exponent over a lane's four head
+// values (zeros give 0)
+__device__ __forceinline__ int head_floor(const fx4& h) {
+    int m = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) m = min(m, __builtin_amdgcn_frexp_expf(h[i]));
+    return m;
+}
+
 __device__ __forceinline__ void zero_tiles(fx4 (&t)[kMaxT]) {
 #pragma unroll
     for (int o = 0; o < kMaxT; ++o) t[o] = fx4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -848,45 +910,61 @@ __device__ __forceinline__ void zero_tiles(fx4 (&t)[kMaxT]) {
 
 // HT: 16-wide output tiles of every hidden layer (1/2/4/8/16); PL: operand planes (3 = bf16x6,
 // 2 = fp16x3, both fp32-class; 1 = plain bf16, inference).
-// NW: waves per workgroup (8: 128-sample tiles, one workgroup per CU; 4: 64-sample tiles, two per
-// CU). Either way two waves share a SIMD and each gets at most 256 registers.
-template <int HT, int PL, int NW>
-__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
+// NW: waves per workgroup; NG: 16-sample groups per wave. (8, 1): 128-sample tiles, one workgroup per
+// CU, two waves per SIMD with at most 256 registers each; (4, 1): 64-sample tiles, two workgroups per
+// CU; (4, 2): 128-sample tiles, ONE wave per SIMD with the whole 512-entry register file, each weight
+// fragment read from LDS feeding both groups' MFMAs (half the LDS bytes per MFMA; fp16x3, HT = 16).
+// A group's logical wave lw = wave NG + group owns samples 16 lw ..+15 of the tile: every slab,
+// shift word, mask word and per-wave minimum keeps the (8, 1) layout, so k2 and the mask readback
+// see the same data whatever NG.
+template <int HT, int PL, int NW, int NG = 1>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NG == 2 ? 1 : 2, NG == 2 ? 1 : 2)))
 k16_fwd_bwd_kernel(K16Args a) {
-    using R = Ring<PL, NW>;
+    using R = Ring<PL, NW, NG>;
+    constexpr int LW = NW * NG;   // logical waves (16-sample groups) per workgroup
     __shared__ __attribute__((aligned(16))) unsigned char lds[R::lds_bytes];
     unsigned char* ring = lds;
     float* comp = (float*)(lds + R::off_comp);
     float* rayloss = (float*)(lds + R::off_ray);
     float* bias_ring = (float*)(lds + R::off_bias);
 
+    if (a.gate && *a.gate == 0) return;   // the floor guard's re-run, not needed this step
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id(), g = lane >> 4, n = lane & 15;
     const int wg = blockIdx.x;
     const int tile_samples = a.rpw * a.S;
-    const int ls = wave * 16 + n;                      // local sample 0..127
 #if LNERF_K16_PRIO
     // static priority for the second-dispatched half (MI355X_MICROARCH.md, two waves per SIMD 4)
     if (wave >= 4) __builtin_amdgcn_s_setprio(1);
 #endif
-    const int gs = wg * tile_samples + ls;             // global sample row (ray*S + j)
-    const bool valid = (ls < tile_samples) && (gs < a.R);
-    const size_t blk = (size_t)wg * (NW / 2) + (wave >> 1);   // 32-sample slab block
-    const int half = wave & 1;
     const bool st = a.want_grad != 0;
+    int lw[NG], ls[NG], gs[NG];
+    bool valid[NG], tail[NG];
+    size_t blk[NG];
+    int half[NG], dmax[NG];
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+        lw[q] = wave * NG + q;
+        ls[q] = lw[q] * 16 + n;                          // local sample 0..127
+        gs[q] = wg * tile_samples + ls[q];               // global sample row (ray*S + j)
+        valid[q] = (ls[q] < tile_samples) && (gs[q] < a.R);
+        blk[q] = (size_t)wg * (LW / 2) + (lw[q] >> 1);   // 32-sample slab block
+        half[q] = lw[q] & 1;
+        // training: this sample is its ray's last (the delta = 1e8 row, train_nerf.py:306-311): kept
+        // out of every layer's product scale E_l and an exceptional row only above it (lnerf_internal.h
+        // kXrowLast); every other row may fall kXrowD0 binades short of E_l before it is one
+        tail[q] = st && valid[q] && !a.head_fit && (ls[q] % a.S) == a.S - 1;
+        dmax[q] = tail[q] ? kXrowLast : kXrowD0;
+    }
 #if LNERF_PROF
     if (lane < 16) prof_slots()[lane] = 0;
     PROF_T(t_start);
     const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
 #endif
 
-    fx4 act[kMaxT], out[kMaxT];
-    zero_tiles(act);
-    ExPack exa;   // training: the forward's A-row shift of this lane's sample, per layer
-    // training: this sample is its ray's last (the delta = 1e8 row, train_nerf.py:306-311): kept out
-    // of every layer's product scale E_l and an exceptional row only above it (lnerf_internal.h
-    // kXrowLast); every other row may fall kXrowD0 binades short of E_l before it is one
-    const bool tail = st && valid && !a.head_fit && (ls % a.S) == a.S - 1;
-    const int dmax = tail ? kXrowLast : kXrowD0;
+    fx4 act[NG][kMaxT], out[NG][kMaxT];
+#pragma unroll
+    for (int q = 0; q < NG; ++q) zero_tiles(act[q]);
+    ExPack exa[NG];   // training: the forward's A-row shift of this lane's sample, per layer
     // PL = 2: layer l's weight exponent shift in lane l (read with readlane per pass); a pass's
     // accumulators carry 2^(ex + ew), removed exactly (powers of two) in its epilogue
     const int wexp_lane = (PL == 2 && lane < a.L) ? wshift_of(a.wexp[lane]) : 0;
@@ -896,38 +974,41 @@ k16_fwd_bwd_kernel(K16Args a) {
         return PL == 2 ? -(ex + __builtin_amdgcn_readlane(wexp_lane, l)) : PL == 3 ? -ex : 0;
     };
 
-    // ---- layer-0 input in the accumulator layout, through a per-wave LDS scratch (the ring is
+    // ---- layer-0 input in the accumulator layout, through a per-group LDS scratch (the ring is
     // free before the first DMA). POINTS/RAYS with k0 <= 64: one lane per (sample, coordinate),
     // comp::encode_coord (pos_encoding.py:54-66); otherwise tile by tile.
-    const int tile_base = wg * tile_samples + wave * 16;
-    if (a.input_mode != LNERF_INPUT_ENCODED && a.k0 <= 64) {
-        constexpr int kStride = 65;
-        float* pe = (float*)ring + wave * (16 * kStride);
-        if (lane < 48) {
-            const int sl = lane / 3, c = lane - 3 * sl;
-            const bool vs = (wave * 16 + sl < tile_samples) && (tile_base + sl < a.R);
-            comp::encode_coord(vs ? comp::sample_coord(a, tile_base + sl, c) : 0.0, a.F, pe + sl * kStride, c);
-        }
-        for (int e = lane; e < 16 * 64; e += 64) {
-            const int sl = e >> 6, f = e & 63;
-            if (f >= a.k0) pe[sl * kStride + f] = 0.0f;
-        }
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
+    for (int q = 0; q < NG; ++q) {
+        const int tile_base = wg * tile_samples + lw[q] * 16;
+        if (a.input_mode != LNERF_INPUT_ENCODED && a.k0 <= 64) {
+            constexpr int kStride = 65;
+            float* pe = (float*)ring + lw[q] * (16 * kStride);
+            if (lane < 48) {
+                const int sl = lane / 3, c = lane - 3 * sl;
+                const bool vs = (lw[q] * 16 + sl < tile_samples) && (tile_base + sl < a.R);
+                comp::encode_coord(vs ? comp::sample_coord(a, tile_base + sl, c) : 0.0, a.F, pe + sl * kStride, c);
+            }
+            for (int e = lane; e < 16 * 64; e += 64) {
+                const int sl = e >> 6, f = e & 63;
+                if (f >= a.k0) pe[sl * kStride + f] = 0.0f;
+            }
 #pragma unroll
-            for (int i = 0; i < 4; ++i) act[t][i] = pe[n * kStride + 16 * t + 4 * g + i];
-    } else {
-        float* pe = (float*)ring + wave * (16 * 17);
+            for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int t = 0; t < kMaxT; ++t) {
-            if (16 * t < a.k0) {
-                for (int e = lane; e < 256; e += 64) {
-                    const int sl = e >> 4, ft = e & 15;
-                    const bool vs = (wave * 16 + sl < tile_samples) && (tile_base + sl < a.R);
-                    pe[sl * 17 + ft] = comp::input_feature(a, tile_base + sl, vs, 16 * t + ft);
+                for (int i = 0; i < 4; ++i) act[q][t][i] = pe[n * kStride + 16 * t + 4 * g + i];
+        } else {
+            float* pe = (float*)ring + lw[q] * (16 * 17);
+#pragma unroll
+            for (int t = 0; t < kMaxT; ++t) {
+                if (16 * t < a.k0) {
+                    for (int e = lane; e < 256; e += 64) {
+                        const int sl = e >> 4, ft = e & 15;
+                        const bool vs = (lw[q] * 16 + sl < tile_samples) && (tile_base + sl < a.R);
+                        pe[sl * 17 + ft] = comp::input_feature(a, tile_base + sl, vs, 16 * t + ft);
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) act[q][t][i] = pe[n * 17 + 4 * g + i];
                 }
-#pragma unroll
-                for (int i = 0; i < 4; ++i) act[t][i] = pe[n * 17 + 4 * g + i];
             }
         }
     }
@@ -937,63 +1018,74 @@ k16_fwd_bwd_kernel(K16Args a) {
     dma_chunk<NW>(a, chunk_at(a, 0), ring, bias_ring);
     dma_barrier(0);
     PROF_ADD(kPfPE, t_start);
-    // ReLU mask bits of this wave, per hidden layer: [L-1][lane] u64
-    unsigned long long* mask_w = a.mask_g + ((size_t)wg * (a.L - 1) * NW + wave) * 64 + lane;
+    // ReLU mask bits of each group, per hidden layer: [L-1][logical wave][lane] u64
+    unsigned long long* mask_w[NG];
+#pragma unroll
+    for (int q = 0; q < NG; ++q) mask_w[q] = a.mask_g + ((size_t)wg * (a.L - 1) * LW + lw[q]) * 64 + lane;
 
     // ---- forward ----
     for (int l = 0; l < a.L; ++l) {
         constexpr int AT = a_tile_floats(PL);   // float slots per activation tile-block (int24: 768)
-        float* slab = !st ? nullptr
-                          : (l == 0 ? a.act + a.x_off + blk * (size_t)(a.kt[0] * AT)
-                                    : a.act + a.act_off[l - 1] + blk * (size_t)(a.kt[l] * AT)) +
-                                half * (AT / 2);
-        zero_tiles(out);
+        float* slab[NG];
+        int ex[NG], sh[NG];
+#pragma unroll
+        for (int q = 0; q < NG; ++q) {
+            slab[q] = !st ? nullptr
+                          : (l == 0 ? a.act + a.x_off + blk[q] * (size_t)(a.kt[0] * AT)
+                                    : a.act + a.act_off[l - 1] + blk[q] * (size_t)(a.kt[l] * AT)) +
+                                half[q] * (AT / 2);
+            zero_tiles(out[q]);
+            const float xm = (PL >= 2 || st) ? sample_max<true>(act[q]) : 0.0f;
+            if (st) exa[q].put(l, store_sexp(a, l, 0, xm, 0, lw[q], LW));
+            ex[q] = shift_of(xm);
+            sh[q] = unscale(l, ex[q]);
+        }
         const float* bl = bias_ring + (l % 3) * 256 + g * 4;
-        const float xm = (PL >= 2 || st) ? sample_max<true>(act) : 0.0f;
-        if (st) exa.put(l, store_sexp(a, l, 0, xm));
-        const int ex = shift_of(xm);
-        const int sh = unscale(l, ex);
         if (l < a.L - 1) {
             PROF_T(t_f);
-            k16_hidden_pass<HT, PL, NW, a24_slabs(PL)>(a, a.ks_f[l], ci, ring, bias_ring, act, out, slab, ex,
-                                                       a.w16 + a.wf_off[l]);
+            k16_hidden_pass<HT, PL, NW, NG, a24_slabs(PL)>(a, a.ks_f[l], ci, ring, bias_ring, act, out, slab, ex,
+                                                           a.w16 + a.wf_off[l]);
             PROF_ADD(kPfFwd, t_f);
             PROF_T(t_fe);
             // bias after the sum (nerf.py:98,125), ReLU (nerf.py:141-144) and its mask bits
             fx4 bv[kMaxT];
             bias_read<HT>(std::make_integer_sequence<int, HT>{}, bl, bv);
-            // values in descending bit order (feature 4o + i ends in bit 4o + i of lo / hi)
-            unsigned mlo = 0u, mhi = 0u;
-            // EPIFMA: unscale and bias as one fma (the scale is a power of two, so out 2^sh is exact
-            // and the sum rounds once either way; only a subnormal out 2^sh would differ, in fma's
-            // favour)
-            const float shs = __builtin_ldexpf(1.0f, sh);
 #pragma unroll
-            for (int o = HT - 1; o >= 0; --o) {
+            for (int q = 0; q < NG; ++q) {
+                // values in descending bit order (feature 4o + i ends in bit 4o + i of lo / hi)
+                unsigned mlo = 0u, mhi = 0u;
+                // EPIFMA: unscale and bias as one fma (the scale is a power of two, so out 2^sh is
+                // exact and the sum rounds once either way; only a subnormal out 2^sh would differ, in
+                // fma's favour)
+                const float shs = __builtin_ldexpf(1.0f, sh[q]);
 #pragma unroll
-                for (int i = 3; i >= 0; --i) {
-                    const float v = LNERF_K16_EPIFMA && PL >= 2
-                                        ? __builtin_fmaf(out[o][i], shs, bv[o][i])
-                                        : (PL >= 2 ? __builtin_ldexpf(out[o][i], sh) : out[o][i]) + bv[o][i];
-                    act[o][i] = relu_bit(v, o >= 8 ? mhi : mlo);
+                for (int o = HT - 1; o >= 0; --o) {
+#pragma unroll
+                    for (int i = 3; i >= 0; --i) {
+                        const float v = LNERF_K16_EPIFMA && PL >= 2
+                                            ? __builtin_fmaf(out[q][o][i], shs, bv[o][i])
+                                            : (PL >= 2 ? __builtin_ldexpf(out[q][o][i], sh[q]) : out[q][o][i]) + bv[o][i];
+                        act[q][o][i] = relu_bit(v, o >= 8 ? mhi : mlo);
+                    }
                 }
+                const unsigned long long mb = ((unsigned long long)mhi << 32) | mlo;
+                if (st) mask_w[q][(size_t)l * LW * 64] = mb;
             }
-
-            const unsigned long long mb = ((unsigned long long)mhi << 32) | mlo;
-            if (st) mask_w[(size_t)l * NW * 64] = mb;
             PROF_ADD(kPfFwdEpi, t_fe);
         } else {
-            k16_pass<1, PL, NW, false, a24_slabs(PL)>(a, a.ks_f[l], ci, ring, bias_ring, act, out, slab, ex);
+            k16_pass<1, PL, NW, NG, false, a24_slabs(PL)>(a, a.ks_f[l], ci, ring, bias_ring, act, out, slab, ex);
             fx4 bv[kMaxT];
             bias_read<1>(std::make_integer_sequence<int, 1>{}, bl, bv);
             // head pre-activations: features 0..3 = registers 0..3 of lane group 0; PL = 2 unscales
             // each column by its own weight shift (head_col_shift)
             if (g == 0) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int shi = PL == 2 ? -(ex + head_col_shift(a.hexp[i], a.wexp[l])) : sh;
-                    comp[ls * 4 + i] = (PL >= 2 ? __builtin_ldexpf(out[0][i], shi) : out[0][i]) + bv[0][i];
-                }
+                for (int q = 0; q < NG; ++q)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int shi = PL == 2 ? -(ex[q] + head_col_shift(a.hexp[i], a.wexp[l])) : sh[q];
+                        comp[ls[q] * 4 + i] = (PL >= 2 ? __builtin_ldexpf(out[q][0][i], shi) : out[q][0][i]) + bv[0][i];
+                    }
             }
         }
     }
@@ -1015,78 +1107,125 @@ k16_fwd_bwd_kernel(K16Args a) {
 
     // ---- reverse chain: G_{L-1} from the head, G_{l-1} = (W_l G_l) * 1[A_{l-1} > 0] ----
     const float* c_gz = comp + 512;
-    zero_tiles(act);
-    if (g == 0 && valid) {
+    // PL = 2, the floor guard (lnerf_internal.h kGuardExp): the smallest frexp exponent over this lane's
+    // elements of the G row the last epilogue produced (zeros give 0), tested against the row's shift
+    // once sample_max has it
+    int gmin[NG];
+    bool below = false;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) act[0][i] = c_gz[ls * 4 + i];
+    for (int q = 0; q < NG; ++q) {
+        gmin[q] = 0;
+        zero_tiles(act[q]);
+        if (g == 0 && valid[q]) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) act[q][0][i] = c_gz[ls[q] * 4 + i];
+        }
     }
     for (int l = a.L - 1; l >= 1; --l) {
-        zero_tiles(out);
-        float* slab = a.grad + a.grad_off[l] + blk * (size_t)(a.nt[l] * 1024) + half * 512;
+        float* slab[NG];
+        int ex[NG], sh[NG];
+        unsigned long long mb[NG];
         PROF_T(t_b);
-        const unsigned long long mb = mask_w[(size_t)(l - 1) * NW * 64];   // in flight over the pass
-        const float xm = sample_max<false>(act);
-        store_emin(a, l, exa.get(l), store_sexp(a, l, 1, xm, dmax), tail);
-        int ex = shift_of(xm);
-        if (PL == 2 && l == a.L - 1) {
-            // the head: G's slab as it is (one k-step), then the pass on the column-scaled G row
-            store_slab_step(slab, act[0], act[1]);
-            slab = nullptr;
-            head_bscale(a, act);
-            ex = shift_of(sample_max<false>(act));
+#pragma unroll
+        for (int q = 0; q < NG; ++q) {
+            zero_tiles(out[q]);
+            slab[q] = a.grad + a.grad_off[l] + blk[q] * (size_t)(a.nt[l] * 1024) + half[q] * 512;
+            mb[q] = mask_w[q][(size_t)(l - 1) * LW * 64];   // in flight over the pass
+            const float xm = sample_max<false>(act[q]);
+            store_emin(a, l, exa[q].get(l), store_sexp(a, l, 1, xm, dmax[q], lw[q], LW), tail[q], lw[q], LW);
+            ex[q] = shift_of(xm);
+            if (PL == 2 && l < a.L - 1) below |= valid[q] && gmin[q] + ex[q] <= kGuardExp;
+            if (PL == 2 && l == a.L - 1) {
+                // the head: G's slab as it is (one k-step), then the pass on the column-scaled G row
+                store_slab_step(slab[q], act[q][0], act[q][1]);
+                slab[q] = nullptr;
+                head_bscale(a, act[q]);
+                ex[q] = shift_of(sample_max<false>(act[q]));
+                // the floor guard on the head row as this pass splits it (column-scaled): an rgb
+                // adjoint 2^40 below a sigma one (delta = 1e8) is gone from every G row below the head
+                below |= valid[q] && head_floor(act[q][0]) + ex[q] <= kGuardExp;
+            }
+            sh[q] = unscale(l, ex[q]);
         }
-        const int sh = unscale(l, ex);
-        k16_hidden_pass<HT, PL, NW>(a, a.ks_b[l], ci, ring, bias_ring, act, out, slab, ex, a.w16 + a.wb_off[l]);
+        k16_hidden_pass<HT, PL, NW, NG>(a, a.ks_b[l], ci, ring, bias_ring, act, out, slab, ex, a.w16 + a.wb_off[l]);
         PROF_ADD(kPfBwd, t_b);
         PROF_T(t_be);
-        // the forward's decision as an all-ones / zero lane mask (v_bfe_i32), one AND per value
-        const int mlo = (int)(unsigned)mb, mhi = (int)(unsigned)(mb >> 32);
 #pragma unroll
-        for (int o = 0; o < HT; ++o)
+        for (int q = 0; q < NG; ++q) {
+            // the forward's decision as an all-ones / zero lane mask (v_bfe_i32), one AND per value
+            const int mlo = (int)(unsigned)mb[q], mhi = (int)(unsigned)(mb[q] >> 32);
+            gmin[q] = 0;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int keep = __builtin_amdgcn_sbfe(o >= 8 ? mhi : mlo, (4 * o + i) & 31, 1);
-                const float g = PL >= 2 ? __builtin_ldexpf(out[o][i], sh) : out[o][i];
-                act[o][i] = __int_as_float(__float_as_int(g) & keep);
-            }
+            for (int o = 0; o < HT; ++o)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int keep = __builtin_amdgcn_sbfe(o >= 8 ? mhi : mlo, (4 * o + i) & 31, 1);
+                    const float gv = PL >= 2 ? __builtin_ldexpf(out[q][o][i], sh[q]) : out[q][o][i];
+                    act[q][o][i] = __int_as_float(__float_as_int(gv) & keep);
+                    if constexpr (PL == 2 && LNERF_GUARD)
+                        gmin[q] = min(gmin[q], __builtin_amdgcn_frexp_expf(act[q][o][i]));
+                }
+        }
         PROF_ADD(kPfBwdEpi, t_be);
     }
     PROF_T(t_t);
     // act holds G_0
-    float* g0 = a.grad + a.grad_off[0] + blk * (size_t)(a.nt[0] * 1024) + half * 512;
+    float* g0[NG];
+#pragma unroll
+    for (int q = 0; q < NG; ++q) g0[q] = a.grad + a.grad_off[0] + blk[q] * (size_t)(a.nt[0] * 1024) + half[q] * 512;
     if (a.d_x) {
         // d_layer_input = G_0 W_0^T (ENCODED mode); the pass also writes G_0's slab
-        zero_tiles(out);
-        const float xm = sample_max<false>(act);
-        store_emin(a, 0, exa.get(0), store_sexp(a, 0, 1, xm, dmax), tail);
-        int ex = shift_of(xm);
-        float* g0s = g0;
-        if (PL == 2 && a.L == 1) {
-            // a head-only MLP: layer 0 is the head (its column-shifted planes, as above)
-            store_slab_step(g0, act[0], act[1]);
-            g0s = nullptr;
-            head_bscale(a, act);
-            ex = shift_of(sample_max<false>(act));
+        float* g0s[NG];
+        int ex[NG], sh[NG];
+#pragma unroll
+        for (int q = 0; q < NG; ++q) {
+            zero_tiles(out[q]);
+            const float xm = sample_max<false>(act[q]);
+            store_emin(a, 0, exa[q].get(0), store_sexp(a, 0, 1, xm, dmax[q], lw[q], LW), tail[q], lw[q], LW);
+            ex[q] = shift_of(xm);
+            if (PL == 2 && a.L > 1) below |= valid[q] && gmin[q] + ex[q] <= kGuardExp;
+            g0s[q] = g0[q];
+            if (PL == 2 && a.L == 1) {
+                // a head-only MLP: layer 0 is the head (its column-shifted planes, as above)
+                store_slab_step(g0[q], act[q][0], act[q][1]);
+                g0s[q] = nullptr;
+                head_bscale(a, act[q]);
+                ex[q] = shift_of(sample_max<false>(act[q]));
+                below |= valid[q] && head_floor(act[q][0]) + ex[q] <= kGuardExp;
+            }
+            sh[q] = unscale(0, ex[q]);
         }
-        const int sh = unscale(0, ex);
-        k16_pass_n<PL, NW>(a, a.ks_b[0], ci, ring, bias_ring, a.to_b[0], act, out, g0s, ex);
-        if (valid) {
+        k16_pass_n<PL, NW, NG>(a, a.ks_b[0], ci, ring, bias_ring, a.to_b[0], act, out, g0s, ex);
 #pragma unroll
-            for (int o = 0; o < kMaxT; ++o)
-                if (16 * o < a.k0) {
+        for (int q = 0; q < NG; ++q) {
+            if (valid[q]) {
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int f = 16 * o + 4 * g + i;
-                        if (f < a.k0) a.d_x[(size_t)gs * a.k0 + f] = PL >= 2 ? __builtin_ldexpf(out[o][i], sh) : out[o][i];
+                for (int o = 0; o < kMaxT; ++o)
+                    if (16 * o < a.k0) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const int f = 16 * o + 4 * g + i;
+                            if (f < a.k0)
+                                a.d_x[(size_t)gs[q] * a.k0 + f] =
+                                    PL >= 2 ? __builtin_ldexpf(out[q][o][i], sh[q]) : out[q][o][i];
+                        }
                     }
-                }
+            }
         }
     } else {
-        store_emin(a, 0, exa.get(0), store_sexp(a, 0, 1, sample_max<false>(act), dmax), tail);
 #pragma unroll
-        for (int s = 0; s < 8; ++s)
-            if (s < a.ks_b[0]) store_slab_step(g0 + s * 1024, act[2 * s], act[2 * s + 1]);
+        for (int q = 0; q < NG; ++q) {
+            const float xm = sample_max<false>(act[q]);
+            store_emin(a, 0, exa[q].get(0), store_sexp(a, 0, 1, xm, dmax[q], lw[q], LW), tail[q], lw[q], LW);
+            if (PL == 2 && a.L > 1) below |= valid[q] && gmin[q] + shift_of(xm) <= kGuardExp;
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+                if (s < a.ks_b[0]) store_slab_step(g0[q] + s * 1024, act[q][2 * s], act[q][2 * s + 1]);
+        }
     }
+    // one plain store per wave that met an element below the floor (every writer stores 1)
+    if (PL == 2 && LNERF_GUARD && a.guard && __builtin_amdgcn_ballot_w64(below) != 0 && lane == 0)
+        *a.guard = 1;
 #if LNERF_PROF
     PROF_ADD(kPfTail, t_t);
     PROF_ADD(kPfTotal, t_start);
@@ -1112,6 +1251,8 @@ struct Pack16Args {
     int* wpart;  // [L][kWmaxParts] partial max|W| bits
     int* hexp;   // planes = 2: the head's per-column max|W| bits [kHeadCols] (pack16_kernel)
     int* hpart;  // [kWmaxParts][kHeadCols] their partials (wmax16_kernel)
+    int* guard_reset;   // nullable: the floor guard's word, zeroed before k1 (lnerf_internal.h kGuardExp)
+    const int* gate;    // nullable: the launch exits at once unless *gate != 0 (the guard's re-run)
 };
 
 // planes = 2: max|W_l| as the bits of a non-negative float (integer order = float order), one
@@ -1154,6 +1295,8 @@ __device__ __forceinline__ int layer_wmax(Pack16Args& a, int l) {
 
 // every layer in one launch: grid (blocks of the largest layer, L)
 __global__ void pack16_kernel(Pack16Args a) {
+    if (a.gate && *a.gate == 0) return;
+    if (a.guard_reset && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.guard_reset = 0;
     const int l = blockIdx.y;
     const float* W = a.W + (size_t)l * a.w_k * a.w_n;
     const int K = a.k[l], N = a.n[l];
@@ -1237,8 +1380,8 @@ unsigned k16_build_knobs() {
            (LNERF_PROF != 0 ? kKnobProf : 0u) | (LNERF_A24 != 1 ? kKnobA24 : 0u) |
            (LNERF_K16_PIN != 2 ? kKnobK16Pin : 0u) | (LNERF_K16_FDSRC != 1 ? kKnobK16FdSrc : 0u) |
            (LNERF_K16_ONECHUNK != 1 ? kKnobK16OneChunk : 0u) | (LNERF_K16_WAVECOMP != 1 ? kKnobK16WaveComp : 0u) |
-           (LNERF_K16_EPIFMA != 1 ? kKnobK16EpiFma : 0u) |
-           (LNERF_PE_DOUBLING != 1 ? kKnobPeDoubling : 0u)
+           (LNERF_K16_EPIFMA != 1 ? kKnobK16EpiFma : 0u) | (LNERF_K16_G2 != 0 ? kKnobK16G2 : 0u) |
+           (LNERF_PE_DOUBLING != 1 ? kKnobPeDoubling : 0u) | (LNERF_GUARD != 1 ? kKnobGuard : 0u)
 #ifdef LNERF_K16_ONLY_16_2
            | kKnobK16Only
 #endif
@@ -1276,6 +1419,8 @@ void k16_pack(const FusedPlan& p, const float* ws, const float* bs, hipStream_t 
     a.wpart = p.wmax_part;
     a.hexp = p.hexp16;
     a.hpart = p.wmax_part + (size_t)kMaxLayers * kWmaxParts;
+    a.guard_reset = p.guard;
+    a.gate = p.gate;
     if (a.planes == 2) wmax16_kernel<<<dim3(kWmaxParts, p.L), 256, 0, s>>>(a);
     size_t nmax = 0;
     for (int l = 0; l < p.L; ++l) {
@@ -1334,6 +1479,8 @@ void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lner
     a.sexp = (unsigned char*)p.sexp;
     a.rpad = p.num_wg * p.tile;
     a.epart = p.epart;
+    a.guard = want_grad && p.x6 == 2 ? p.guard : nullptr;
+    a.gate = p.gate;
     // the chunk stream: forward 0..L-1, backward L-1..1 (training), backward 0 (d_x); chunks of
     // KC k-steps (Ring: 2 for fp16x3 / bf16, 1 for bf16x6), the pack layout's consecutive k-steps
     {
@@ -1355,6 +1502,13 @@ void k16_launch(const FusedPlan& p, const lnerf_batch& b, float seed, const lner
         // a zero entry past the end (the kernel looks one chunk ahead): a{} zeroed it
     }
     static_assert(sizeof(K16Args) <= 4096, "kernel arguments");
+#if LNERF_K16_G2
+    // two 16-sample groups per wave, one wave per SIMD (fp16x3, 256-wide hidden layers, 128-sample tiles)
+    if (p.x6 == 2 && p.tile == 128 && p.ht16 == 16) {
+        k16_fwd_bwd_kernel<16, 2, 4, 2><<<p.num_wg, 256, 0, s>>>(a);
+        return;
+    }
+#endif
 #ifdef LNERF_K16_ONLY_16_2   // compile-time experiments: one instantiation
     if (p.tile == 64) k16_fwd_bwd_kernel<16, 2, 4><<<p.num_wg, 256, 0, s>>>(a);
     else k16_fwd_bwd_kernel<16, 2, 8><<<p.num_wg, 512, 0, s>>>(a);

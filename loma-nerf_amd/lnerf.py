@@ -47,6 +47,7 @@ EXPORTED_SYMBOLS = [
     "lnerf_workspace_bytes", "lnerf_train_step", "lnerf_render", "lnerf_scale_by_device_scalar",
     "lnerf_adam_update", "lnerf_ctx_timings", "lnerf_get_rays", "lnerf_ctx_last_path",
     "lnerf_ctx_set_option", "lnerf_ctx_relu_masks", "lnerf_build_knobs", "lnerf_ctx_exceptional_rows",
+    "lnerf_ctx_guard_fired",
 ]
 
 # lnerf_ctx_last_path bits
@@ -168,10 +169,12 @@ def configure(lib: ctypes.CDLL) -> None:
     if hasattr(lib, "lnerf_ctx_exceptional_rows"):   # (older in-tree A/B builds lack it)
         lib.lnerf_ctx_exceptional_rows.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong),
                                                    ctypes.POINTER(ctypes.c_longlong)]
+    if hasattr(lib, "lnerf_ctx_guard_fired"):   # (round 6; older A/B builds lack it)
+        lib.lnerf_ctx_guard_fired.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
     lib.lnerf_get_rays.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(ctypes.c_double), ctypes.c_void_p, ctypes.c_void_p]
     for name in ("lnerf_ctx_timings", "lnerf_ctx_last_path", "lnerf_ctx_set_option", "lnerf_ctx_relu_masks",
-                 "lnerf_ctx_exceptional_rows",
+                 "lnerf_ctx_exceptional_rows", "lnerf_ctx_guard_fired",
                  "lnerf_ctx_create", "lnerf_train_step", "lnerf_render",
                  "lnerf_scale_by_device_scalar", "lnerf_adam_update", "lnerf_get_rays"):
         if hasattr(lib, name):
@@ -354,6 +357,15 @@ class Engine:
         if self.lib.lnerf_ctx_exceptional_rows(self.ctx, ctypes.byref(n), ctypes.byref(t)) != 0:
             raise RuntimeError(f"lnerf_ctx_exceptional_rows: {last_error()}")
         return (int(n.value), int(t.value)) if split else int(n.value)
+
+    def guard_fired(self):
+        """The last training step's fp16x3 floor guard (lnerf_ctx_guard_fired; synchronises): 1 if k1
+        found a hidden G element below fp16x3's floor and the step re-ran on the bf16x6 split, 0 if
+        not, -1 if the step had no guard (an explicit precision flag, the generic path, ...)."""
+        f = ctypes.c_int(0)
+        if self.lib.lnerf_ctx_guard_fired(self.ctx, ctypes.byref(f)) != 0:
+            raise RuntimeError(f"lnerf_ctx_guard_fired: {last_error()}")
+        return int(f.value)
 
     def last_path(self) -> dict:
         """The kernels the last train_step/render ran (lnerf_ctx_last_path)."""

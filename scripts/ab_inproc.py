@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--block", type=int, default=8)
     ap.add_argument("--config", default="cfg3")
     ap.add_argument("--render", action="store_true", help="the config-5 frame (kr) instead of cfg3 training")
+    ap.add_argument("--lr", type=float, default=None,
+                    help="Adam learning rate (0: the weights never move, so timing-knob builds with wrong "
+                         "gradients keep running on the same sane weights as the product)")
     a = ap.parse_args()
     import torch
     import bench
@@ -47,6 +50,8 @@ def main():
     sys.argv = [saved[0]]   # bench.py's defaults (RAYS input, Adam in the step)
     args = bench.parse()
     sys.argv = saved
+    if a.lr is not None:
+        args.lr = a.lr
     if a.render:
         return render_ab(a, LibEngine)
     trainers = []

@@ -124,7 +124,7 @@ def render_np(X, ws, bs, dists, S, operands=None):
 
 def bf16_render_bound(X, ws, bs, dists, S, colour, K_acc=256, sigmas=6.0, floor=1e-4):
     """Per-element error model of kr's colours against float64, derived like
-    test_gpu_edge.fp16x3_dw_bound from the operand format: bf16 keeps 8 significant bits
+    the fp16x3 split bounds of earlier rounds from the operand format: bf16 keeps 8 significant bits
     (u = 2^-8 relative per rounded operand), products of two bf16 are exact in fp32 and summed in
     fp32 (gamma = K_acc 2^-24 of the sum of |terms|). Layer l's pre-activation z_l[s, n] carries a
     local error
@@ -202,6 +202,46 @@ def test_kr_vs_float64_per_element(engine):
     err = np.abs(got - ref)
     print(f"kr vs bf16-operand float64: max err {err_emu.max():.3g}; vs float64: max err {err.max():.3g}, "
           f"max err / bound {(err / bound).max():.3g}, median bound {np.median(bound):.3g}")
+    assert np.isfinite(got).all()
+    assert err_emu.max() <= 3e-4, err_emu.max()
+    assert (err <= bound).all(), float((err / bound).max())
+
+
+def test_kr_config5_frame_subset_vs_float64(engine):
+    """the config-5 workload itself -- the 800x800 frame at 128 samples through
+    kr (what bench.py --render times) -- checked on a seeded subset of 512 of its rays, every
+    channel, against the float64 restatement: within 3e-4 of the bf16-operand emulation (kr's own
+    arithmetic with exact sums) and within bf16_render_bound of plain float64 (train_nerf.py:616-662,
+    scripts/nerf.py:67-288)."""
+    import lnerf
+    import nerf_np
+    import scene
+    import torch
+    S = 128
+    shapes, wp, bp = scene.init_mlp(33, 4, 8, 256)
+    mlp = lnerf.make_mlp(shapes, wp.shape[1], wp.shape[2])
+    focal = 0.5 / np.tan(0.5 * scene.CAMERA_ANGLE_X)
+    K = np.array([[focal, 0, 0.5], [0, focal, 0.5], [0, 0, 1]])
+    rays = engine.get_rays(800, K, scene.look_at_pose())
+    tgt = torch.zeros(rays.shape[0], 3, dtype=torch.float32, device="cuda:0")
+    _, acc = engine.render(mlp, _dev(wp), _dev(bp), rays, None, tgt, samples=S, input_mode=lnerf.INPUT_RAYS,
+                           flags=lnerf.FAST | lnerf.MFMA_BF16)
+    assert engine.last_path()["kr"]
+    torch.cuda.synchronize()
+    sel = np.sort(np.random.RandomState(5).choice(rays.shape[0], 512, replace=False))
+    got = acc.cpu().numpy().astype(np.float64)[sel]
+    r = rays.cpu().numpy().astype(np.float64)[sel]
+    pts, dists = nerf_np.sample_rays(r[:, :3], r[:, 3:], S)
+    X = nerf_np.positional_encoding_3d(pts, 5).reshape(-1, 33)
+    dists = dists.astype(np.float32)
+    ws = [wp[l, :k, :n] for l, (k, n) in enumerate(shapes)]
+    bs = [bp[l, :n] for l, (_, n) in enumerate(shapes)]
+    emu, _ = render_np(X, ws, bs, dists, S, operands="bf16")
+    ref, _ = render_np(X, ws, bs, dists, S)
+    bound = bf16_render_bound(X, ws, bs, dists, S, ref)
+    err_emu, err = np.abs(got - emu), np.abs(got - ref)
+    print(f"config-5 frame, 512-ray subset: kr vs bf16-operand float64 max err {err_emu.max():.3g}; vs float64 "
+          f"max err {err.max():.3g}, max err / bound {(err / bound).max():.3g}")
     assert np.isfinite(got).all()
     assert err_emu.max() <= 3e-4, err_emu.max()
     assert (err <= bound).all(), float((err / bound).max())

@@ -265,9 +265,9 @@ int lnerf_ctx_exceptional_rows(lnerf_ctx* ctx, long long* rows, long long* last_
 /* The fp16x3 floor guard of the last training step on `ctx`: *fired = 1 if k1 met a hidden-layer
  * gradient element below what the fp16x3 split can carry (more than ~2^37 below its row's maximum,
  * lnerf_internal.h kGuardExp) and the step was therefore re-run on the device on the bf16x6 split
- * (every output of the step comes from that re-run), 0 if not, -1 if the step had no guard (an
- * explicit precision flag, the generic path, LNERF_HEAD_FIT or LNERF_K16_W4). Synchronises the
- * device. An extension (no loma counterpart). */
+ * (every output of the step comes from that re-run), 0 if not, -1 if the last call on `ctx` had no
+ * guard (a training step with an explicit precision flag, the generic path, LNERF_HEAD_FIT or
+ * LNERF_K16_W4; a render). Synchronises the device. An extension (no loma counterpart). */
 int lnerf_ctx_guard_fired(lnerf_ctx* ctx, int* fired);
 
 /* Sets an engine option (LNERF_OPT_*) for later steps on `ctx`. Returns 0, or a negative code for

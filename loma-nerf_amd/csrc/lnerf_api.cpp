@@ -718,8 +718,11 @@ extern "C" int lnerf_train_step(lnerf_ctx* ctx, const lnerf_mlp* mlp, const floa
                 fused_plan(px, *mlp, *batch, wsb, flags | LNERF_MFMA_BF16X6, true, ctx->dw_grid);
                 px.guard = nullptr;
                 px.gate = p.guard;
+                px.w16 = p.w16x;   // packed by p's own pack launch, beside its fp16x3 planes
+                px.w16x = nullptr;
             } else {
                 p.guard = nullptr;
+                p.w16x = nullptr;
             }
             const bool timed = (flags & LNERF_TIMING) != 0;
             fused_train_step(p, ws, bs, *batch, seed, flags, o, s, timed ? ctx->ev : nullptr, guarded ? &px : nullptr);
@@ -763,6 +766,8 @@ extern "C" int lnerf_render(lnerf_ctx* ctx, const lnerf_mlp* mlp, const float* w
             const size_t bytes = fused_workspace_bytes(*mlp, batch->rays, batch->samples, false, ctx->dw_grid);
             FusedPlan p{};
             fused_plan(p, *mlp, *batch, ctx->fused_ws.get(bytes), flags, false, ctx->dw_grid);
+            p.guard = nullptr;   // (the floor guard is a training-step feature)
+            p.w16x = nullptr;
             const bool timed = (flags & LNERF_TIMING) != 0;
             fused_render(p, ws, bs, *batch, o, s, flags, timed ? ctx->ev : nullptr);
             ctx->timed = timed;
@@ -841,9 +846,9 @@ extern "C" int lnerf_ctx_guard_fired(lnerf_ctx* ctx, int* fired) {
     return guard_int([&]() {
         if (!ctx || !fired) fail("null argument");
         std::lock_guard<std::mutex> lock(ctx->mu);
-        if (!ctx->last_k16_train) fail("no k16 training step has run on this context since the last other call");
+        *fired = -1;   // no guard on the last call (the generic path, a render, an explicit precision)
+        if (!ctx->last_k16_train) return;
         const FusedPlan& p = ctx->last_plan;
-        *fired = -1;   // no guard on that step (not the default fp16x3 precision)
         if (!p.guard) return;
         HIP_OK(hipSetDevice(ctx->device));
         HIP_OK(hipDeviceSynchronize());

@@ -85,11 +85,6 @@ struct ReduceArgs {
     float* d_bs;
     const float* scale;          // nullable device scalar (seed = loss)
     int accumulate;
-    // the floor guard (lnerf_internal.h kGuardExp): with gate set, the launch runs only when
-    // (*gate != 0) == gate_want -- the fp16x3 partials' reduction when the guard stayed clear, the
-    // bf16x6 re-run's when it fired
-    const int* gate;
-    int gate_want;
 };
 
 // In-order sum of n strided partials (deterministic); loads are issued 8 at a time so the
@@ -109,7 +104,6 @@ __device__ __forceinline__ float sum_parts(const float* __restrict__ p, size_t s
 }
 
 __global__ void grad_reduce_kernel(ReduceArgs a) {
-    if (a.gate && ((*a.gate != 0) ? 1 : 0) != a.gate_want) return;
     const size_t nW = (size_t)a.L * a.w_k * a.w_n, nB = (size_t)a.L * a.w_n;
     const float sc = a.scale ? *a.scale : 1.0f;
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < nW + nB;
@@ -253,7 +247,7 @@ static size_t workspace_floats(const lnerf_mlp& m, int rays, int S, bool train, 
     make_layout(y, m, rays, S, train, dw_grid, tile);
     return 64 + align_up(y.act_total, 64) + align_up(y.grad_total, 64) + align_up((size_t)y.num_wg, 64) +
            align_up(y.dwp_total, 64) + align_up(y.dbp_total, 64) + 64 + align_up((size_t)kLossStage1, 64) +
-           align_up((y.w16_total + 1) / 2, 64) +
+           2 * align_up((y.w16_total + 1) / 2, 64) +   // + the guard's bf16x6 planes
            align_up(y.b16_total, 64) + align_up(y.mask_total * 2, 64) + 64 +   // + the fp16x3 shifts
            align_up((size_t)kMaxLayers * kWmaxParts + kWmaxParts * kHeadCols, 64) +   // per-block max|W|
            align_up((size_t)kHeadCols, 64) +                                     // head column max|W|
@@ -329,6 +323,7 @@ static void fused_plan_tile(FusedPlan& p, const lnerf_mlp& m, const lnerf_batch&
     p.loss_total = take(1);
     p.loss_stage = take(kLossStage1);
     p.w16 = (unsigned short*)take((y.w16_total + 1) / 2);
+    p.w16x = (unsigned short*)take((y.w16_total + 1) / 2);
     p.b16 = take(y.b16_total);
     p.mask_g = (unsigned long long*)take(y.mask_total * 2);
     p.wexp16 = (int*)take(2 * kMaxLayers);
@@ -400,26 +395,18 @@ void fused_train_step(const FusedPlan& p, const float* ws, const float* bs, cons
     mark(3);
     dw16_launch(p, s);
     mark(4);
-    ReduceArgs ra = reduce_args(p, out, flags);
     if (px && p.guard) {
-        // the floor guard (lnerf_internal.h kGuardExp): this reduction runs only if k1 left the guard
-        // clear; otherwise the same step again on the bf16x6 split (px: the same workspace, every
-        // pointer but the activation slabs shared), each kernel exiting at once while the guard is
-        // clear, and its reduction in place of this one
-        ra.gate = p.guard;
-        ra.gate_want = 0;
-        grad_reduce_kernel<<<rgrid, 256, 0, s>>>(ra);
-        k16_pack(*px, ws, bs, s);
+        // the floor guard (lnerf_internal.h kGuardExp): the same step again on the bf16x6 split (px:
+        // the same workspace, every pointer but the activation slabs shared, the dW/db partials
+        // included), each kernel exiting at once while k1 left the guard clear; the one reduction
+        // below then sums whichever partials the last dW kernel wrote
+        // (px's bf16x6 planes came out of p's pack: k16_pack wrote both formats)
         k16_launch(*px, b, seed_loss ? 1.0f : seed, out, true, s);
         k1_reduce_launch(*px, out.loss, s);
         dw16_launch(*px, s);
-        ReduceArgs rx = reduce_args(*px, out, flags);
-        rx.gate = p.guard;
-        rx.gate_want = 1;
-        grad_reduce_kernel<<<rgrid, 256, 0, s>>>(rx);
-    } else {
-        grad_reduce_kernel<<<rgrid, 256, 0, s>>>(ra);
     }
+    const ReduceArgs ra = reduce_args(p, out, flags);
+    grad_reduce_kernel<<<rgrid, 256, 0, s>>>(ra);
     if (seed_loss) {
         if (out.d_dists) k_scale_by_scalar(out.d_dists, (size_t)p.R, p.loss_total, s);
         if (out.d_target)

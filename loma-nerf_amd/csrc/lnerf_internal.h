@@ -228,6 +228,8 @@ struct FusedPlan {
     int ks16_f[kMaxLayers], ks16_b[kMaxLayers];   // k-steps (32 features) per pass
     int to16_f[kMaxLayers], to16_b[kMaxLayers];   // 16-wide output tiles per pass
     unsigned short* w16;                 // packed planes, u16 offsets below
+    unsigned short* w16x;                // nullable: the bf16x6 planes of the floor guard's re-run, written by
+                                         // the fp16x3 step's own pack (same offsets, three planes)
     size_t w16f_off[kMaxLayers], w16b_off[kMaxLayers];
     float* b16;                          // [L][256] zero-padded biases
     unsigned long long* mask_g;          // [num_wg][L-1][waves][64 lanes] ReLU mask bits

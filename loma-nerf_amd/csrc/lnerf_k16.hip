@@ -1252,6 +1252,7 @@ struct Pack16Args {
     int* hexp;   // planes = 2: the head's per-column max|W| bits [kHeadCols] (pack16_kernel)
     int* hpart;  // [kWmaxParts][kHeadCols] their partials (wmax16_kernel)
     int* guard_reset;   // nullable: the floor guard's word, zeroed before k1 (lnerf_internal.h kGuardExp)
+    unsigned short* w16x;   // nullable (planes = 2): also the bf16x6 planes of the guard's re-run, three planes
     const int* gate;    // nullable: the launch exits at once unless *gate != 0 (the guard's re-run)
 };
 
@@ -1338,6 +1339,16 @@ __global__ void pack16_kernel(Pack16Args a) {
             split_h(__builtin_ldexpf(w, head && jj < kHeadCols ? hsh[jj] : wsh), h, lo);
             dst[0] = __builtin_bit_cast(unsigned short, h);
             dst[512] = __builtin_bit_cast(unsigned short, lo);
+            if (a.w16x) {
+                // the floor guard's re-run reads these (no pack launch of its own)
+                unsigned short* dx = a.w16x + (fwd ? a.wf_off[l] : a.wb_off[l]) + ((size_t)(s * to + o) * 3) * 512 +
+                                     ln * 8 + j;
+                __bf16 xh, xm, xl;
+                split_x(w, xh, xm, xl);
+                dx[0] = __builtin_bit_cast(unsigned short, xh);
+                dx[512] = __builtin_bit_cast(unsigned short, xm);
+                dx[1024] = __builtin_bit_cast(unsigned short, xl);
+            }
             continue;
         }
         __bf16 h, mi, lo;
@@ -1421,6 +1432,7 @@ void k16_pack(const FusedPlan& p, const float* ws, const float* bs, hipStream_t 
     a.hpart = p.wmax_part + (size_t)kMaxLayers * kWmaxParts;
     a.guard_reset = p.guard;
     a.gate = p.gate;
+    a.w16x = p.x6 == 2 ? p.w16x : nullptr;
     if (a.planes == 2) wmax16_kernel<<<dim3(kWmaxParts, p.L), 256, 0, s>>>(a);
     size_t nmax = 0;
     for (int l = 0; l < p.L; ++l) {

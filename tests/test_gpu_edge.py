@@ -123,6 +123,19 @@ def test_edge_numerics(engine, name, prec):
     assert (np.sign(got["d_dists"][sub]) == np.sign(g["d_dists"][sub])).all()
 
 
+def test_floor_guard_only_under_the_default_precision(engine):
+    """The floor guard (lnerf_internal.h kGuardExp) belongs to the default precision: an explicit
+    LNERF_MFMA_F16X3 runs fp16x3 exactly (no re-run; lnerf_ctx_guard_fired reports -1) and so do the
+    other explicit precisions and the generic path; the default on the same fixture fires it."""
+    import lnerf
+    g = load("edge_finite_6x8.npz")
+    for flags in (lnerf.MFMA_F16X3, lnerf.MFMA_BF16X6, lnerf.GENERIC):
+        run(engine, g, flags)
+        assert engine.guard_fired() == -1, flags
+    run(engine, g, 0)
+    assert engine.guard_fired() == 1
+
+
 @pytest.mark.parametrize("prec", list(PRECS))
 def test_nan_input_row_propagates(engine, prec):
     """a NaN in the encoded input (ENCODED mode, the loma layer_input) must leave dW
